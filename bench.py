@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Benchmark of the epoch-to-feature hot path (BASELINE.json metric, configs[1] per GPU).
+
+One step = one launch of the fused raw -> dwt-8 feature kernel over one batch of 1,000,000
+synthetic epochs (3 channels, multiplexed int16 @ 1000 Hz, one marker every 1000 frames),
+inputs already resident in HBM.  N GPUs = N ranks (torch.distributed, RCCL), each with its own
+recording of the same shape (weak scaling: epochs are independent, no data-path collective).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--numerics exact|fma]
+
+Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").  Extra legs:
+  roofline      algorithmic bytes per launch / average launch duration, measured with HIP
+                events on the stream the kernel runs on, against 8.0 TB/s (MI355X_MICROARCH.md);
+                traffic from the committed rocprofv3 PMC summary when one matches (else null);
+  cpu_baseline  the C restatement (oracle/, reference-faithful full pyramid) timed on the host
+                cores on a bounded sample of the same workload (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "epochs/sec feature-extracted (whole node) + % HBM roofline, 1/2/4/8 GPUs"
+BYTES_PER_EPOCH = 612 * 3 * 2 + 8 + 48 * 8   # 3,672 in + 8 marker + 384 out
+HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
+SEED = 0x5EED
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
+    ap.add_argument("--numerics", choices=["exact", "fma"], default="exact")
+    ap.add_argument("--cpu-sample", type=int, default=100_000,
+                    help="epochs in the CPU-baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather leg")
+    return ap.parse_args()
+
+
+def traffic_from_profiles(workload_key):
+    """HBM bytes per launch from the committed PMC summary (profiles/*traffic*.json)."""
+    best = None
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir)):
+        if f.endswith(".json") and "traffic" in f:
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except Exception:
+                continue
+            if d.get("workload_key") == workload_key and d.get("hbm_bytes_per_launch"):
+                best = d
+    return best
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    distributed = world > 1
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import eeg_dataanalysispackage_amd as fx
+
+    n = args.epochs
+    n_frames = FRAMES_PER_EPOCH * n + 2000
+    ctx = fx.Context(local, numerics=args.numerics)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)  # kernels run on torch's stream: events see them
+
+    raw = torch.empty((n_frames, 3), dtype=torch.int16, device=dev)
+    ctx.synth_recording(raw, 3, SEED + rank)
+    pos = torch.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (n + 1), FRAMES_PER_EPOCH,
+                       dtype=torch.int64, device=dev)
+    out = torch.empty((n, 48), dtype=torch.float64, device=dev)
+    cols, res = [0, 1, 2], [0.1, 0.1, 0.1]
+
+    def step():
+        ctx.process_recording(raw, 3, cols, res, pos, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # average launch duration on its stream
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    # sanity of the produced features (unit rows) -- outside the timed region
+    norms = torch.linalg.vector_norm(out, dim=1)
+    ok_norm = bool(torch.all(torch.isfinite(norms)) and torch.max(torch.abs(norms - 1)) < 1e-12)
+
+    gather = None
+    if distributed and not args.no_gather:
+        # RCCL over xGMI only moves the feature matrices: all-gather into rank order.
+        full = torch.empty((world * n, 48), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(full, out)  # warm
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        dist.all_gather_into_tensor(full, out)
+        torch.cuda.synchronize(dev)
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather = {"op": "all_gather_into_tensor", "bytes_per_rank": n * 48 * 8,
+                  "ms": round(float(gt[0]) * 1e3, 3)}
+        del full
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(args, raw, out)
+
+    if rank == 0:
+        workload_key = f"fused_dwt8_c3_int16_{n}_{args.numerics}"
+        value = world * n * args.steps / elapsed
+        launch_bytes = n * BYTES_PER_EPOCH
+        achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        prof = traffic_from_profiles(workload_key)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "epochs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "configs[1]: synthetic 1M epochs x 3 ch (Fz/Cz/Pz) multiplexed int16 "
+                            "@1000 Hz -> fe=dwt-8 48-dim L2-normalised features, per GPU",
+                "epochs_per_gpu": n,
+                "channels": 3,
+                "numerics": args.numerics,
+                "kernel": "fused_features_kernel<3,3>",
+                "unit_rows_check": ok_norm,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": (round(prof["hbm_bytes_per_launch"]) if prof else None),
+                "kernel_ms": round(kernel_ms, 4),
+                "bytes_per_epoch": BYTES_PER_EPOCH,
+            },
+            "cpu_baseline": cpu,
+        }
+        if gather:
+            line["gather"] = gather
+        print(json.dumps(line), flush=True)
+
+    ctx.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, raw, gpu_out):
+    """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
+    threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload."""
+    from oracle import oracle
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    k = min(args.cpu_sample, args.epochs)
+    host = raw[: FRAMES_PER_EPOCH * k + 2000].cpu().numpy()
+    pos = np.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (k + 1), FRAMES_PER_EPOCH, dtype=np.int64)
+    oracle.process_recording(host[: FRAMES_PER_EPOCH * 200 + 2000], [0, 1, 2], [0.1] * 3,
+                             pos[:200], faithful=True, nthreads=threads)  # warm-up
+    t0 = time.perf_counter()
+    feats = oracle.process_recording(host, [0, 1, 2], [0.1] * 3, pos, faithful=True,
+                                     nthreads=threads)
+    dt = time.perf_counter() - t0
+    gpu = gpu_out[:k].cpu().numpy()
+    if args.numerics == "exact":
+        parity = bool(np.array_equal(gpu, feats, equal_nan=True))
+    else:
+        parity = bool(np.max(np.abs(gpu - feats)) <= 1e-9)
+    return {
+        "value": round(k / dt, 1),
+        "unit": "epochs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {k} epochs of the rank-0 synthetic recording, C restatement of the "
+                  f"Java path (full 6-level pyramid), {threads} threads over contiguous ranges, "
+                  f"{dt:.2f} s wall",
+        "gpu_parity_on_sample": parity,
+    }
+
+
+if __name__ == "__main__":
+    main()

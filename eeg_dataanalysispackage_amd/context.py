@@ -1,0 +1,174 @@
+"""Device context and the compute entry points of libeegfx (include/eegfx.h).
+
+Arrays may be numpy arrays (host memory: the library stages them through HBM and returns after
+the results are copied back) or torch tensors on a ROCm device (device memory: the work is
+enqueued on the context stream and the call returns without synchronising).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_float, c_int, c_int64, c_void_p
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+
+def _is_device(a) -> bool:
+    return hasattr(a, "is_cuda") and a.is_cuda
+
+
+def _mem(*arrays) -> int:
+    kinds = {_is_device(a) for a in arrays if a is not None}
+    if len(kinds) != 1:
+        raise ValueError("all buffers of one call must live in the same memory (host or device)")
+    return _lib.MEM_DEVICE if kinds.pop() else _lib.MEM_HOST
+
+
+def _contig(a, dtype):
+    if _is_device(a):
+        if not a.is_contiguous():
+            raise ValueError("device tensors must be contiguous")
+        return a
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class Context:
+    """One HIP device + stream (eegfx_ctx).  numerics: "exact" (bit-exact to the reference
+    order of operations, default) or "fma" (fused multiply-add filter bank, <= 1e-9 relative)."""
+
+    def __init__(self, device: int = 0, numerics: str = "exact"):
+        h = c_void_p()
+        check(lib().eegfx_ctx_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.set_numerics(numerics)
+
+    # -- context ----------------------------------------------------------------------------------
+    @property
+    def handle(self) -> c_void_p:
+        if self._h is None:
+            raise RuntimeError("context destroyed")
+        return self._h
+
+    def set_numerics(self, numerics: str) -> None:
+        mode = {"exact": _lib.EXACT, "fma": _lib.FMA}[numerics]
+        check(lib().eegfx_ctx_set_numerics(self.handle, mode))
+        self.numerics = numerics
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        check(lib().eegfx_ctx_set_stream(self.handle, c_void_p(stream_handle or 0)))
+
+    def set_timing(self, enable: bool) -> None:
+        check(lib().eegfx_ctx_set_timing(self.handle, 1 if enable else 0))
+
+    def synchronize(self) -> None:
+        check(lib().eegfx_ctx_synchronize(self.handle))
+
+    def last_kernel_ms(self) -> float:
+        ms = c_float()
+        check(lib().eegfx_ctx_last_kernel_ms(self.handle, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            lib().eegfx_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- compute ----------------------------------------------------------------------------------
+    @staticmethod
+    def _sel(cols: Sequence[int], res: Sequence[float]):
+        cols_a = np.ascontiguousarray(cols, dtype=np.int32)
+        res_a = np.ascontiguousarray(res, dtype=np.float32)
+        if cols_a.shape != res_a.shape or cols_a.ndim != 1:
+            raise ValueError("cols and res must be 1-D of equal length")
+        return cols_a, res_a
+
+    def cut_epochs(self, raw, n_channels_total: int, cols, res, pos, out=None):
+        """Raw multiplexed recording (int16 or float32, n_frames x n_channels_total) ->
+        baseline-corrected epochs double[n][C][750] (OffLineDataProvider.java:216-233)."""
+        cols_a, res_a = self._sel(cols, res)
+        fmt = _fmt(raw)
+        n_frames = _numel(raw) // n_channels_total
+        pos = _contig(pos, np.int64)
+        n = _numel(pos)
+        C = len(cols_a)
+        if out is None:
+            out = _empty_like_mem(raw, (n, C, _lib.POSTSTIMULUS), "float64")
+        mem = _mem(raw, pos, out)
+        check(lib().eegfx_cut_epochs_f64(self.handle, ptr(raw), fmt, n_frames, n_channels_total,
+                                         ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out), mem))
+        return out
+
+    def extract_features(self, epochs, name=8, epoch_size=512, skip=175, feature_size=16,
+                         out=None):
+        """Batched WaveletTransform.extractFeatures over epochs double[n][C][750]."""
+        epochs = _contig(epochs, np.float64)
+        shape = tuple(epochs.shape)
+        if len(shape) != 3 or shape[2] != _lib.POSTSTIMULUS:
+            raise ValueError(f"epochs must be [n][C][750], got {shape}")
+        n, C = shape[0], shape[1]
+        if out is None:
+            out = _empty_like_mem(epochs, (n, C * feature_size), "float64")
+        mem = _mem(epochs, out)
+        check(lib().eegfx_extract_features_f64(self.handle, ptr(epochs), n, C, name, epoch_size,
+                                               skip, feature_size, ptr(out), mem))
+        return out
+
+    def process_recording(self, raw, n_channels_total: int, cols, res, pos, out=None):
+        """Fused hot path: raw recording + marker positions -> dwt-8 features [n][16*C]."""
+        cols_a, res_a = self._sel(cols, res)
+        fmt = _fmt(raw)
+        n_frames = _numel(raw) // n_channels_total
+        pos = _contig(pos, np.int64)
+        n = _numel(pos)
+        C = len(cols_a)
+        if out is None:
+            out = _empty_like_mem(raw, (n, 16 * C), "float64")
+        mem = _mem(raw, pos, out)
+        check(lib().eegfx_process_recording(self.handle, ptr(raw), fmt, n_frames,
+                                            n_channels_total, ptr(cols_a), ptr(res_a), C,
+                                            ptr(pos), n, ptr(out), mem))
+        return out
+
+    def synth_recording(self, dst, n_channels: int, seed: int) -> None:
+        """Fills a device int16 tensor (n_frames x n_channels) with the synthetic recording."""
+        if not _is_device(dst):
+            raise ValueError("synth_recording writes a device tensor")
+        n_frames = dst.numel() // n_channels
+        check(lib().eegfx_synth_recording(self.handle, ptr(dst), n_frames, n_channels,
+                                          ctypes.c_uint64(seed)))
+
+
+def device_count() -> int:
+    n = c_int()
+    check(lib().eegfx_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _numel(a) -> int:
+    return int(a.numel()) if hasattr(a, "numel") and callable(a.numel) else int(np.asarray(a).size)
+
+
+def _fmt(raw) -> int:
+    name = str(raw.dtype)
+    if name.endswith("int16"):
+        return _lib.INT_16
+    if name.endswith("float32"):
+        return _lib.IEEE_FLOAT_32
+    raise ValueError(f"raw samples must be int16 or float32, got {raw.dtype}")
+
+
+def _empty_like_mem(ref, shape, dtype: str):
+    if _is_device(ref):
+        import torch
+        return torch.empty(shape, dtype=getattr(torch, dtype), device=ref.device)
+    return np.empty(shape, dtype=dtype)

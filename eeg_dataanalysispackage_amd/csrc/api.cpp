@@ -1,0 +1,647 @@
+// api.cpp -- eegfx C ABI: device context, compute entry points and the OffLineDataProvider.
+//
+// The data provider mirrors DataTransformation/OffLineDataProvider.java (constructor :78,
+// loadData :88-98, handleInput :111-141, processEEGFiles :147-268, loadFilesFromInfoTxt
+// :283-319, setFileNames :327-365, getData :370, getDataLabels :377) with local files in place
+// of HDFS.  Epochs are cut and baseline-corrected on the GPU and stay resident in HBM; getData()
+// copies them back on demand.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "launch.h"
+
+using namespace eegfx;
+
+#define HIP_CHECK(expr)                                                                 \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) fail(EEGFX_EHIP, "%s: %s", #expr, hipGetErrorString(_e));     \
+  } while (0)
+
+namespace {
+
+// Grow-only device allocation owned by a context.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* get(size_t bytes) {
+    if (bytes > cap) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        p = nullptr;
+        fail(EEGFX_ENOMEM, "hipMalloc(%zu) failed", bytes);
+      }
+      cap = bytes;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+ChanSel make_sel(const int32_t* cols, const float* res, int C, int ct) {
+  if (C < 1 || C > kMaxChannels) fail(EEGFX_EINVAL, "C=%d outside [1, %d]", C, kMaxChannels);
+  if (!cols || !res) fail(EEGFX_EINVAL, "cols/res must be host arrays");
+  ChanSel s;
+  memset(&s, 0, sizeof(s));
+  for (int c = 0; c < C; ++c) {
+    if (cols[c] < 0 || cols[c] >= ct)
+      fail(EEGFX_EINVAL, "column %d of selected channel %d outside [0, %d)", cols[c], c, ct);
+    s.col[c] = cols[c];
+    s.res[c] = res[c];
+  }
+  return s;
+}
+
+void check_positions(const int64_t* pos, int64_t n, int64_t n_frames) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t lo = pos[i] - EEGFX_PRESTIMULUS;
+    if (lo < 0 || lo > n_frames)
+      fail(EEGFX_ERANGE, "epoch %lld: marker position %lld outside [100, %lld]", (long long)i,
+           (long long)pos[i], (long long)n_frames + EEGFX_PRESTIMULUS);
+  }
+}
+
+void check_fe_params(int C, int name, int epoch_size, int skip, int feature_size) {
+  if (C < 1 || C > kMaxChannels) fail(EEGFX_EINVAL, "C=%d outside [1, %d]", C, kMaxChannels);
+  if (skip < 0 || epoch_size <= 0 || skip + epoch_size > EEGFX_POSTSTIMULUS)
+    fail(EEGFX_ERANGE, "window [%d, %d) outside the %d-sample epoch", skip, skip + epoch_size,
+         EEGFX_POSTSTIMULUS);
+  if (feature_size <= 0) fail(EEGFX_EINVAL, "feature size %d", feature_size);
+  if (name != EEGFX_DWT8_NAME || epoch_size != EEGFX_DWT8_EPOCH_SIZE || feature_size > 16)
+    fail(EEGFX_ENOTSUP,
+         "no kernel for wavelet %d / epoch size %d / feature size %d (supported: dwt-8, 512, <=16)",
+         name, epoch_size, feature_size);
+}
+
+}  // namespace
+
+struct eegfx_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int numerics = EEGFX_EXACT;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool have_time = false;
+  DevBuf raw, pos, out, scratch;
+
+  void activate() const { HIP_CHECK(hipSetDevice(device)); }
+  void tic() {
+    if (timing) HIP_CHECK(hipEventRecord(ev0, stream));
+  }
+  void toc() {
+    if (timing) {
+      HIP_CHECK(hipEventRecord(ev1, stream));
+      have_time = true;
+    }
+  }
+};
+
+namespace {
+
+void* stage_in(eegfx_ctx* ctx, DevBuf& buf, const void* src, size_t bytes, int mem) {
+  if (mem == EEGFX_MEM_DEVICE) return const_cast<void*>(src);
+  void* d = buf.get(bytes);
+  if (bytes) HIP_CHECK(hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return d;
+}
+
+void check_mem(int mem) {
+  if (mem != EEGFX_MEM_HOST && mem != EEGFX_MEM_DEVICE) fail(EEGFX_EINVAL, "mem flag %d", mem);
+}
+
+// raw -> features on the context stream (device pointers).  Fused kernel when one covers the
+// layout, otherwise cut + features through the context scratch buffer.
+void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_frames, int ct,
+                           const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                           double* out) {
+  const bool fast = ctx->numerics == EEGFX_FMA;
+  ctx->tic();
+  hipError_t e = launch_fused_features(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast, out);
+  if (e == hipErrorNotSupported) {
+    (void)hipGetLastError();
+    double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
+    HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep));
+    e = launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
+                                    EEGFX_DWT8_FEATURE_SIZE, fast, out);
+  }
+  HIP_CHECK(e);
+  ctx->toc();
+}
+
+}  // namespace
+
+// ================================================================================================
+// OffLineDataProvider
+// ================================================================================================
+struct eegfx_odp {
+  eegfx_ctx* ctx = nullptr;
+  std::vector<std::string> args;
+  std::string error;
+  // Map<String, Integer> files = new LinkedHashMap<>() (:54): insertion order, put() on an
+  // existing key keeps the position and replaces the value.
+  std::vector<std::pair<std::string, int32_t>> files;
+  std::string file_prefix;
+  std::string vhdr_file, vmrk_file, eeg_file;
+  int32_t fz_index = 0, cz_index = 0, pz_index = 0;  // fields: persist across files (:49-51)
+  int64_t balance = 0;                                // numberOfTargets - numberOfNonTargets
+  int64_t epochs_counter = 0;
+  std::vector<double> labels;
+  std::vector<int64_t> positions;
+  std::vector<int32_t> file_of_epoch;
+  DevBuf d_epochs;   // double[n][3][750], resident
+  int64_t n_epochs = 0;
+
+  void put_file(const std::string& k, int32_t v) {
+    for (auto& kv : files)
+      if (kv.first == k) {
+        kv.second = v;
+        return;
+      }
+    files.emplace_back(k, v);
+  }
+
+  static bool ends_with_4(const std::string& s, const char* suf) {
+    // fileLocation.substring(fileLocation.length() - 4): StringIndexOutOfBounds below 4 chars.
+    if (s.size() < 4) fail(EEGFX_EINVAL, "String index out of range: %d", (int)s.size() - 4);
+    return s.compare(s.size() - 4, 4, suf) == 0;
+  }
+
+  void handle_input() {  // :111-141
+    if (args.empty() || args.size() > 6)
+      fail(EEGFX_EINVAL,
+           "Please enter the input in one of these formats: 1. <location of info.txt file> "
+           "2. <location of a .eeg file> <guessed number>  *<optional values>");
+    const std::string& loc = args[0];
+    if (ends_with_4(loc, ".eeg")) {
+      file_prefix = "";
+      if (args.size() < 2) fail(EEGFX_EINVAL, "Index 1 out of bounds for length 1");
+      int32_t g;
+      if (!java_parse_int(args[1], &g))
+        fail(EEGFX_EFORMAT, "For input string: \"%s\"", args[1].c_str());
+      put_file(loc, g);
+    } else if (ends_with_4(loc, ".txt")) {
+      const size_t slash = loc.rfind('/');
+      if (slash == std::string::npos) fail(EEGFX_EINVAL, "String index out of range: -1");
+      file_prefix = loc.substr(0, slash) + "/";
+      load_files_from_info_txt(loc);
+    } else {
+      fail(EEGFX_EINVAL,
+           "Please enter the input in one of these formats: 1. <location of info.txt file> "
+           "2. <location of a .eeg file> <target number>  *<optional values>");
+    }
+  }
+
+  void load_files_from_info_txt(const std::string& loc) {  // :283-319
+    FILE* f = fopen(loc.c_str(), "rb");
+    if (!f) fail(EEGFX_EIO, "File %s does not exist", loc.c_str());
+    std::string text;
+    char buf[4096];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, r);
+    fclose(f);
+    std::vector<std::string> lines;
+    std::string cur;
+    for (size_t i = 0; i < text.size(); ++i) {  // BufferedReader.readLine
+      const char ch = text[i];
+      if (ch == '\n' || ch == '\r') {
+        lines.push_back(cur);
+        cur.clear();
+        if (ch == '\r' && i + 1 < text.size() && text[i + 1] == '\n') ++i;
+      } else {
+        cur.push_back(ch);
+      }
+    }
+    if (!cur.empty()) lines.push_back(cur);
+    for (const std::string& line : lines) {
+      if (line.empty() || line[0] == '#') continue;
+      std::vector<std::string> parts = java_split_space(line);
+      if (parts.size() > 1) {
+        int32_t num;
+        if (!java_parse_int(parts[1], &num))
+          fail(EEGFX_EFORMAT, "Line %s contains an improper number format", line.c_str());
+        put_file(parts[0], num);
+      }
+    }
+  }
+
+  // setFileNames (:327-365): false = the reference's caught IllegalArgumentException (skip file).
+  bool set_file_names(const std::string& loc, std::string* why) {
+    if (loc.size() <= 4) {
+      *why = "Incorrect file name, must be at least longer than 4 characters ";
+      return false;
+    }
+    if (loc.compare(loc.size() - 4, 4, ".eeg") != 0) {
+      *why = "Invalid .eeg file";
+      return false;
+    }
+    const std::string base = loc.substr(0, loc.rfind('.'));
+    const std::string vhdr = base + ".vhdr", vmrk = base + ".vmrk";
+    if (!file_exists(vhdr)) {
+      *why = "No related .vhdr file found for the original .eeg file " + vhdr;
+      return false;
+    }
+    if (!file_exists(vmrk)) {
+      *why = "No related .vmrk file found for the original .eeg file " + vmrk;
+      return false;
+    }
+    if (!file_exists(loc)) {
+      *why = "No related .eeg file found for the original .eeg file " + loc;
+      return false;
+    }
+    vhdr_file = vhdr;
+    vmrk_file = vmrk;
+    eeg_file = loc;
+    return true;
+  }
+
+  void append_epochs(const Header& h, int64_t n_frames, const void* d_raw,
+                     const std::vector<int64_t>& pos, int32_t file_idx,
+                     const std::vector<double>& lab) {
+    const int64_t k = (int64_t)pos.size();
+    if (k == 0) return;
+    if (!ctx) {  // planning-only provider: selection, labels and offsets without epochs
+      n_epochs += k;
+      positions.insert(positions.end(), pos.begin(), pos.end());
+      labels.insert(labels.end(), lab.begin(), lab.end());
+      file_of_epoch.insert(file_of_epoch.end(), (size_t)k, file_idx);
+      return;
+    }
+    const int ct = h.info.n_channels;
+    int32_t cols[3];
+    float res[3];
+    const int32_t idx[3] = {fz_index, cz_index, pz_index};
+    for (int c = 0; c < 3; ++c) {
+      cols[c] = idx[c] - 1;
+      res[c] = 1.0f;
+      for (const auto& ci : h.channels)
+        if (ci.number == idx[c]) res[c] = (float)ci.resolution;
+    }
+    const ChanSel sel = make_sel(cols, res, 3, ct);
+    const size_t per = sizeof(double) * 3 * EEGFX_POSTSTIMULUS;
+    // grow the resident epoch buffer (copy-on-grow)
+    const size_t need = per * (size_t)(n_epochs + k);
+    if (need > d_epochs.cap) {
+      size_t cap = std::max(need, d_epochs.cap * 2);
+      void* np = nullptr;
+      HIP_CHECK(hipMalloc(&np, cap));
+      if (n_epochs)
+        HIP_CHECK(hipMemcpyAsync(np, d_epochs.p, per * (size_t)n_epochs, hipMemcpyDeviceToDevice,
+                                 ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      d_epochs.release();
+      d_epochs.p = np;
+      d_epochs.cap = cap;
+    }
+    int64_t* d_pos = (int64_t*)ctx->pos.get(sizeof(int64_t) * (size_t)k);
+    HIP_CHECK(hipMemcpyAsync(d_pos, pos.data(), sizeof(int64_t) * (size_t)k,
+                             hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, h.info.binary_format, n_frames, ct, sel, 3,
+                                d_pos, k, (double*)((char*)d_epochs.p + per * (size_t)n_epochs)));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    n_epochs += k;
+    positions.insert(positions.end(), pos.begin(), pos.end());
+    labels.insert(labels.end(), lab.begin(), lab.end());
+    file_of_epoch.insert(file_of_epoch.end(), (size_t)k, file_idx);
+  }
+
+  void process_eeg_files() {  // :147-268
+    int32_t file_idx = -1;
+    for (const auto& entry : files) {
+      ++file_idx;
+      std::string why;
+      if (!set_file_names(file_prefix + entry.first, &why)) continue;  // logged + skipped (:157-161)
+      const Header h = read_header(vhdr_file);
+      for (const auto& ch : h.channels) {  // :172-183
+        std::string name = ch.name;
+        for (auto& c : name) c = (char)tolower((unsigned char)c);
+        if (name == "fz") fz_index = ch.number;
+        else if (name == "cz") cz_index = ch.number;
+        if (name == "pz") pz_index = ch.number;
+      }
+      if (!h.info.multiplexed)
+        fail(EEGFX_ENOTSUP, "%s: VECTORIZED data orientation is not supported", vhdr_file.c_str());
+      const int32_t sel[3] = {fz_index, cz_index, pz_index};
+      for (int c = 0; c < 3; ++c)
+        if (sel[c] < 1 || sel[c] > h.info.n_channels)
+          fail(EEGFX_EINVAL, "%s: channel %s not found (index %d)", vhdr_file.c_str(),
+               c == 0 ? "Fz" : c == 1 ? "Cz" : "Pz", sel[c]);
+      const int64_t n_frames = recording_frames(h, eeg_file);
+      const size_t raw_bytes =
+          (size_t)n_frames * h.info.n_channels * sample_bytes(h.info.binary_format);
+      void* d_raw = nullptr;
+      if (ctx) {  // planning-only providers (no context) never touch the recording payload
+        std::vector<char> host(raw_bytes);
+        read_file_bytes(eeg_file, host.data(), (int64_t)raw_bytes);
+        d_raw = ctx->raw.get(raw_bytes);
+        HIP_CHECK(hipMemcpyAsync(d_raw, host.data(), raw_bytes, hipMemcpyHostToDevice,
+                                 ctx->stream));
+      }
+
+      const std::vector<eegfx_marker> markers = read_markers(vmrk_file);
+      std::vector<int64_t> pos(markers.size());
+      std::vector<double> lab(markers.size());
+      int64_t k = 0;
+      const int rc = eegfx_plan_markers(markers.data(), (int64_t)markers.size(), n_frames,
+                                        entry.second, &balance, pos.data(), lab.data(), &k);
+      pos.resize((size_t)k);
+      lab.resize((size_t)k);
+      epochs_counter += k;
+      append_epochs(h, n_frames, d_raw, pos, file_idx, lab);  // epochs accepted before an error
+      if (rc != EEGFX_OK) fail(rc, "%s", last_error().c_str());
+    }
+  }
+};
+
+extern "C" {
+
+const char* eegfx_version(void) { return "eegfx 0.1.0 (gfx950)"; }
+
+int eegfx_device_count(int* count) {
+  return guarded([&] {
+    if (!count) fail(EEGFX_EINVAL, "null argument");
+    HIP_CHECK(hipGetDeviceCount(count));
+  });
+}
+
+int eegfx_ctx_create(int device, eegfx_ctx** out) {
+  return guarded([&] {
+    if (!out) fail(EEGFX_EINVAL, "null argument");
+    std::unique_ptr<eegfx_ctx> c(new eegfx_ctx());
+    c->device = device;
+    c->activate();
+    HIP_CHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    c->stream = c->own;
+    HIP_CHECK(hipEventCreate(&c->ev0));
+    HIP_CHECK(hipEventCreate(&c->ev1));
+    *out = c.release();
+  });
+}
+
+int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own;
+  });
+}
+
+int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    if (numerics != EEGFX_EXACT && numerics != EEGFX_FMA) fail(EEGFX_EINVAL, "numerics %d", numerics);
+    ctx->numerics = numerics;
+  });
+}
+
+int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    ctx->timing = enable != 0;
+    ctx->have_time = false;
+  });
+}
+
+int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    ctx->activate();
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int eegfx_ctx_last_kernel_ms(eegfx_ctx* ctx, float* ms) {
+  return guarded([&] {
+    if (!ctx || !ms) fail(EEGFX_EINVAL, "null argument");
+    if (!ctx->have_time) fail(EEGFX_EINVAL, "no timed launch (enable eegfx_ctx_set_timing)");
+    HIP_CHECK(hipEventSynchronize(ctx->ev1));
+    HIP_CHECK(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+  });
+}
+
+int eegfx_ctx_destroy(eegfx_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->own);
+    ctx->raw.release();
+    ctx->pos.release();
+    ctx->out.release();
+    ctx->scratch.release();
+    (void)hipEventDestroy(ctx->ev0);
+    (void)hipEventDestroy(ctx->ev1);
+    (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+  });
+}
+
+int eegfx_read_raw(eegfx_ctx* ctx, const char* vhdr_path, const char* eeg_path, void* dst,
+                   int64_t capacity_bytes, int mem) {
+  return guarded([&] {
+    if (!vhdr_path || !eeg_path || !dst) fail(EEGFX_EINVAL, "null argument");
+    check_mem(mem);
+    const Header h = read_header(vhdr_path);
+    const int64_t n = recording_frames(h, eeg_path);
+    const int64_t bytes = n * h.info.n_channels * sample_bytes(h.info.binary_format);
+    if (bytes > capacity_bytes)
+      fail(EEGFX_EINVAL, "capacity %lld < %lld bytes", (long long)capacity_bytes, (long long)bytes);
+    if (mem == EEGFX_MEM_HOST) {
+      read_file_bytes(eeg_path, dst, bytes);
+    } else {
+      if (!ctx) fail(EEGFX_EINVAL, "device read needs a context");
+      ctx->activate();
+      std::vector<char> host((size_t)bytes);
+      read_file_bytes(eeg_path, host.data(), bytes);
+      HIP_CHECK(hipMemcpyAsync(dst, host.data(), (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+  });
+}
+
+int eegfx_cut_epochs_f64(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                         int32_t ct, const int32_t* cols, const float* res, int32_t C,
+                         const int64_t* pos, int64_t n, double* epochs_out, int mem) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    check_mem(mem);
+    if (fmt != EEGFX_INT_16 && fmt != EEGFX_IEEE_FLOAT_32) fail(EEGFX_EINVAL, "format %d", fmt);
+    if (n_frames < 0 || n < 0 || ct < 1) fail(EEGFX_EINVAL, "negative size");
+    if (n > 0 && (!raw || !pos || !epochs_out)) fail(EEGFX_EINVAL, "null buffer");
+    const ChanSel sel = make_sel(cols, res, C, ct);
+    if (mem == EEGFX_MEM_HOST) check_positions(pos, n, n_frames);
+    if (n == 0) return;
+    ctx->activate();
+    const size_t raw_bytes = (size_t)n_frames * ct * (fmt == EEGFX_INT_16 ? 2 : 4);
+    const size_t out_bytes = sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS;
+    const void* d_raw = stage_in(ctx, ctx->raw, raw, raw_bytes, mem);
+    const int64_t* d_pos = (const int64_t*)stage_in(ctx, ctx->pos, pos, sizeof(int64_t) * n, mem);
+    double* d_out = mem == EEGFX_MEM_DEVICE ? epochs_out : (double*)ctx->out.get(out_bytes);
+    ctx->tic();
+    HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out));
+    ctx->toc();
+    if (mem == EEGFX_MEM_HOST) {
+      HIP_CHECK(hipMemcpyAsync(epochs_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+  });
+}
+
+int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, int32_t C,
+                               int32_t name, int32_t epoch_size, int32_t skip,
+                               int32_t feature_size, double* out, int mem) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    check_mem(mem);
+    check_fe_params(C, name, epoch_size, skip, feature_size);
+    if (n < 0) fail(EEGFX_EINVAL, "negative count");
+    if (n == 0) return;
+    if (!epochs || !out) fail(EEGFX_EINVAL, "null buffer");
+    ctx->activate();
+    const size_t in_bytes = sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS;
+    const size_t out_bytes = sizeof(double) * (size_t)n * C * feature_size;
+    const double* d_in = (const double*)stage_in(ctx, ctx->scratch, epochs, in_bytes, mem);
+    double* d_out = mem == EEGFX_MEM_DEVICE ? out : (double*)ctx->out.get(out_bytes);
+    ctx->tic();
+    HIP_CHECK(launch_features_from_epochs(ctx->stream, d_in, n, C, skip, feature_size,
+                                          ctx->numerics == EEGFX_FMA, d_out));
+    ctx->toc();
+    if (mem == EEGFX_MEM_HOST) {
+      HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+  });
+}
+
+int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                            int32_t ct, const int32_t* cols, const float* res, int32_t C,
+                            const int64_t* pos, int64_t n, double* features, int mem) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    check_mem(mem);
+    if (fmt != EEGFX_INT_16 && fmt != EEGFX_IEEE_FLOAT_32) fail(EEGFX_EINVAL, "format %d", fmt);
+    if (n_frames < 0 || n < 0 || ct < 1) fail(EEGFX_EINVAL, "negative size");
+    if (n > 0 && (!raw || !pos || !features)) fail(EEGFX_EINVAL, "null buffer");
+    const ChanSel sel = make_sel(cols, res, C, ct);
+    if (mem == EEGFX_MEM_HOST) check_positions(pos, n, n_frames);
+    if (n == 0) return;
+    ctx->activate();
+    const size_t raw_bytes = (size_t)n_frames * ct * (fmt == EEGFX_INT_16 ? 2 : 4);
+    const size_t out_bytes = sizeof(double) * (size_t)n * C * EEGFX_DWT8_FEATURE_SIZE;
+    const void* d_raw = stage_in(ctx, ctx->raw, raw, raw_bytes, mem);
+    const int64_t* d_pos = (const int64_t*)stage_in(ctx, ctx->pos, pos, sizeof(int64_t) * n, mem);
+    double* d_out = mem == EEGFX_MEM_DEVICE ? features : (double*)ctx->out.get(out_bytes);
+    run_features_from_raw(ctx, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out);
+    if (mem == EEGFX_MEM_HOST) {
+      HIP_CHECK(hipMemcpyAsync(features, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+  });
+}
+
+int eegfx_synth_recording(eegfx_ctx* ctx, int16_t* dst, int64_t n_frames, int32_t n_channels,
+                          uint64_t seed) {
+  return guarded([&] {
+    if (!ctx || !dst) fail(EEGFX_EINVAL, "null argument");
+    if (n_frames < 0 || n_channels < 1) fail(EEGFX_EINVAL, "bad size");
+    ctx->activate();
+    HIP_CHECK(launch_synth(ctx->stream, dst, n_frames, n_channels, seed));
+  });
+}
+
+// ---- OffLineDataProvider ----------------------------------------------------------------------
+int eegfx_odp_create(eegfx_ctx* ctx, const char* const* args, int32_t n_args, eegfx_odp** out) {
+  return guarded([&] {
+    if (!out || (n_args > 0 && !args) || n_args < 0) fail(EEGFX_EINVAL, "null argument");
+    std::unique_ptr<eegfx_odp> o(new eegfx_odp());
+    o->ctx = ctx;
+    for (int i = 0; i < n_args; ++i) o->args.emplace_back(args[i] ? args[i] : "");
+    *out = o.release();
+  });
+}
+
+int eegfx_odp_load_data(eegfx_odp* odp) {
+  if (!odp) {
+    set_last_error("null provider");
+    return EEGFX_EINVAL;
+  }
+  // loadData (:88-98): every exception is logged as fatal and swallowed; what was loaded stays.
+  const int rc = guarded([&] {
+    if (odp->ctx) odp->ctx->activate();
+    odp->handle_input();
+    odp->process_eeg_files();
+  });
+  odp->error = rc == EEGFX_OK ? "" : last_error();
+  return rc;
+}
+
+const char* eegfx_odp_error(const eegfx_odp* odp) { return odp ? odp->error.c_str() : "null provider"; }
+
+int64_t eegfx_odp_num_epochs(const eegfx_odp* odp) { return odp ? odp->n_epochs : 0; }
+
+int eegfx_odp_get_data(const eegfx_odp* odp, double* out) {
+  return guarded([&] {
+    if (!odp || !out) fail(EEGFX_EINVAL, "null argument");
+    if (!odp->n_epochs) return;
+    if (!odp->ctx) fail(EEGFX_EINVAL, "planning-only provider (no device context) holds no epochs");
+    odp->ctx->activate();
+    HIP_CHECK(hipMemcpyAsync(out, odp->d_epochs.p,
+                             sizeof(double) * 3 * EEGFX_POSTSTIMULUS * (size_t)odp->n_epochs,
+                             hipMemcpyDeviceToHost, odp->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(odp->ctx->stream));
+  });
+}
+
+int eegfx_odp_get_labels(const eegfx_odp* odp, double* out) {
+  return guarded([&] {
+    if (!odp || !out) fail(EEGFX_EINVAL, "null argument");
+    std::copy(odp->labels.begin(), odp->labels.end(), out);
+  });
+}
+
+int eegfx_odp_get_positions(const eegfx_odp* odp, int64_t* pos_out, int32_t* file_out) {
+  return guarded([&] {
+    if (!odp) fail(EEGFX_EINVAL, "null argument");
+    if (pos_out) std::copy(odp->positions.begin(), odp->positions.end(), pos_out);
+    if (file_out) std::copy(odp->file_of_epoch.begin(), odp->file_of_epoch.end(), file_out);
+  });
+}
+
+int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int32_t skip,
+                           int32_t feature_size, double* out) {
+  return guarded([&] {
+    if (!odp || !out) fail(EEGFX_EINVAL, "null argument");
+    check_fe_params(3, name, epoch_size, skip, feature_size);
+    if (!odp->n_epochs) return;
+    if (!odp->ctx) fail(EEGFX_EINVAL, "planning-only provider (no device context) holds no epochs");
+    eegfx_ctx* ctx = odp->ctx;
+    ctx->activate();
+    const size_t out_bytes = sizeof(double) * (size_t)odp->n_epochs * 3 * feature_size;
+    double* d_out = (double*)ctx->out.get(out_bytes);
+    HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)odp->d_epochs.p,
+                                          odp->n_epochs, 3, skip, feature_size,
+                                          ctx->numerics == EEGFX_FMA, d_out));
+    HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+void eegfx_odp_destroy(eegfx_odp* odp) {
+  if (!odp) return;
+  if (odp->ctx) (void)hipSetDevice(odp->ctx->device);
+  odp->d_epochs.release();
+  delete odp;
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// dwt8.h -- the fe=dwt-8 filter bank as a per-lane device routine for gfx950 (wave64).
+//
+// Reference: FeatureExtraction/WaveletTransform.java:126-137 runs the eegdsp 1.0 DWT
+// (names[8]; un-vendored jar, pom.xml:79-83) on x = epoch[c][175..686] and keeps the first 16
+// coefficients.  SURVEY.md Appendix A pins that transform: 10-tap Daubechies filter with
+// 12-decimal literals, periodic extension, pyramid while n >= 10 (512 -> 256 -> ... -> 16), the
+// first 16 coefficients are a6[0..7] ++ d6[0..7].
+//
+// MI355X mapping.  One (epoch, channel) signal is owned by an aligned group of 8 lanes of one
+// wave.  Lane s holds samples [64s, 64s+64) plus an 8-sample halo, and at every level owns the
+// matching contiguous slice of the coefficients:
+//     level  1   2   3   4   5   6
+//     owned 32  16   8   4   2   1(a6) + 1(d6)
+// so every lane computes exactly 64 outputs (perfect balance, no idle lanes at the deep
+// levels).  Between levels each lane publishes the head of its slice in a per-lane LDS slot and
+// reads the 8-value halo of the next level from the lanes that follow it (periodic wrap inside
+// the group = the reference's periodic extension).  Everything else stays in VGPRs; only the
+// detail coefficients that reach the output (d6) are ever computed (5,120 MAC per channel
+// instead of the reference's 10,080).
+//
+// Numerics.  EXACT: every tap is one rounded fp64 multiply followed by one rounded fp64 add in
+// the reference's j = 0..9 order (the file is compiled with -ffp-contract=off), which makes the
+// coefficients bit-identical to the Java/C restatement up to the sign of an exactly-zero sum
+// (the reference starts its accumulator at +0.0).  FMA: the same chain with
+// fused multiply-adds (within 1e-9 relative of EXACT, tested).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace eegfx {
+namespace dev {
+
+constexpr int kPre = 100;   // Const.PREESTIMULUS_VALUES
+constexpr int kPost = 750;  // Const.POSTSTIMULUS_VALUES
+constexpr int kWin = 512;   // WaveletTransform EPOCH_SIZE for dwt-8
+constexpr int kTaps = 10;
+constexpr int kLanesPerSignal = 8;
+constexpr int kSegLen = kWin / kLanesPerSignal;  // 64 samples per lane
+constexpr int kIn = kSegLen + 8;                 // + halo
+constexpr int kSlot = 10;  // doubles per lane exchange slot (80 B: conflict-free ds_read_b128)
+
+// Low-pass taps.  High-pass g[j] = (-1)^(j+1) h[9-j].
+#define EEGFX_H0 0.160102397974
+#define EEGFX_H1 0.603829269797
+#define EEGFX_H2 0.724308528438
+#define EEGFX_H3 0.138428145901
+#define EEGFX_H4 -0.242294887066
+#define EEGFX_H5 -0.032244869585
+#define EEGFX_H6 0.077571493840
+#define EEGFX_H7 -0.006241490213
+#define EEGFX_H8 -0.012580751999
+#define EEGFX_H9 0.003335725285
+
+__device__ __forceinline__ constexpr double tap_h(int j) {
+  return j == 0 ? EEGFX_H0 : j == 1 ? EEGFX_H1 : j == 2 ? EEGFX_H2 : j == 3 ? EEGFX_H3
+       : j == 4 ? EEGFX_H4 : j == 5 ? EEGFX_H5 : j == 6 ? EEGFX_H6 : j == 7 ? EEGFX_H7
+       : j == 8 ? EEGFX_H8 : EEGFX_H9;
+}
+__device__ __forceinline__ constexpr double tap_g(int j) {
+  return (j & 1) ? tap_h(kTaps - 1 - j) : -tap_h(kTaps - 1 - j);
+}
+
+// One output of the analysis filter: sum_j x[j] * f[j], j = 0..9, in order.
+template <bool FAST, bool HIGH>
+__device__ __forceinline__ double fir10(const double* x) {
+  double a = x[0] * (HIGH ? tap_g(0) : tap_h(0));
+#pragma unroll
+  for (int j = 1; j < kTaps; ++j) {
+    const double t = HIGH ? tap_g(j) : tap_h(j);
+    if constexpr (FAST) a = __builtin_fma(x[j], t, a);
+    else a = a + x[j] * t;
+  }
+  return a;
+}
+
+template <int N, bool FAST>
+__device__ __forceinline__ void lowpass(const double* in, double* out) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = fir10<FAST, false>(in + 2 * i);
+}
+
+// Orders LDS traffic of the lanes of one wave (DS ops of a wave execute in order; the fences
+// keep the compiler from moving them across this point).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Publishes the first min(CNT, 8) owned values v[0..) and gathers the 8 values that follow the
+// lane's slice at this level into v[CNT .. CNT+8) from lanes s+1, s+2, ... (mod 8).
+template <int CNT>
+__device__ __forceinline__ void halo_exchange(double* v, double* xch, int gbase, int s) {
+  constexpr int P = CNT < 8 ? CNT : 8;
+  double* mine = xch + (gbase + s) * kSlot;
+#pragma unroll
+  for (int i = 0; i < P; ++i) mine[i] = v[i];
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int src = (s + 1 + m / P) & (kLanesPerSignal - 1);
+    v[CNT + m] = xch[(gbase + src) * kSlot + (m % P)];
+  }
+  wave_sync();
+}
+
+// x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
+// xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
+// Returns a6[s] and d6[s].
+template <bool FAST>
+__device__ __forceinline__ void dwt8_cascade(const double (&x)[kIn], double* xch, int gbase, int s,
+                                             double& a6, double& d6) {
+  double a1[32 + 8];
+  lowpass<32, FAST>(x, a1);
+  halo_exchange<32>(a1, xch, gbase, s);
+  double a2[16 + 8];
+  lowpass<16, FAST>(a1, a2);
+  halo_exchange<16>(a2, xch, gbase, s);
+  double a3[8 + 8];
+  lowpass<8, FAST>(a2, a3);
+  halo_exchange<8>(a3, xch, gbase, s);
+  double a4[4 + 8];
+  lowpass<4, FAST>(a3, a4);
+  halo_exchange<4>(a4, xch, gbase, s);
+  double a5[2 + 8];
+  lowpass<2, FAST>(a4, a5);
+  halo_exchange<2>(a5, xch, gbase, s);
+  a6 = fir10<FAST, false>(a5);
+  d6 = fir10<FAST, true>(a5);
+}
+
+}  // namespace dev
+}  // namespace eegfx

@@ -1,0 +1,182 @@
+// kernels.hip -- gfx950 kernels of the epoch-to-feature path and their launchers.
+//
+//   cut_epochs_kernel            a3 + a5..a7: raw multiplexed samples -> baseline-corrected
+//                                epochs double[n][C][750]  (OffLineDataProvider.java:216-233)
+//   features_from_epochs_kernel  a11..a13: epochs -> L2-normalised dwt-8 features
+//                                (WaveletTransform.java:107-141, SignalProcessing.java:38-52)
+//   fused kernel                 see fused.hip (raw -> features, the benchmarked hot path)
+//   synth_kernel                 deterministic synthetic recordings for tests and bench.py
+//
+// Compiled with -ffp-contract=off: every fp32/fp64 expression is evaluated as written, one
+// correctly rounded IEEE operation at a time, matching the Java (strictfp-equivalent) order.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dwt8.h"
+#include "launch.h"
+
+namespace eegfx {
+namespace dev {
+
+// a3 + a5..a7.  One workgroup per epoch.  Lanes 0..C-1 fold the 100 pre-stimulus samples of
+// their channel sequentially in fp32 (Baseline.java:29-42 -- order-exact, so no tree reduction),
+// then all lanes write the 750 post-stimulus samples, coalesced.
+template <typename T>
+__global__ __launch_bounds__(256) void cut_epochs_kernel(const T* __restrict__ raw, int64_t n_frames,
+                                                         int ct, ChanSel sel, int C,
+                                                         const int64_t* __restrict__ pos,
+                                                         double* __restrict__ out) {
+  __shared__ float base[kMaxChannels];
+  const int64_t e = blockIdx.x;
+  const int64_t p = pos[e];
+  const int64_t lo = p - kPre;
+  if ((int)threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const int col = sel.col[c];
+    const float r = sel.res[c];
+    float b = 0.0f;
+    for (int i = 0; i < kPre; ++i) {
+      const int64_t f = lo + i;
+      // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f).
+      const float v = (f >= 0 && f < n_frames) ? (float)raw[f * ct + col] * r : 0.0f;
+      b = b + v;
+    }
+    base[c] = b / (float)kPre;
+  }
+  __syncthreads();
+  double* o = out + e * C * kPost;
+  for (int idx = threadIdx.x; idx < C * kPost; idx += blockDim.x) {
+    const int c = idx / kPost;
+    const int64_t f = p + (idx - c * kPost);
+    const float v = (f >= 0 && f < n_frames) ? (float)raw[f * ct + sel.col[c]] * sel.res[c] : 0.0f;
+    o[idx] = (double)(v - base[c]);
+  }
+}
+
+// a11..a13 from materialised epochs.  A workgroup owns 8 epochs; wave w walks the channels
+// w, w+NW, ...; within a wave lane = 8*epoch + segment (dwt8.h).  Features are collected in LDS,
+// normalised per epoch with the reference's sequential sum of squares, and written coalesced.
+template <bool FAST>
+__global__ __launch_bounds__(256) void features_from_epochs_kernel(const double* __restrict__ ep,
+                                                                   int64_t n, int C, int skip,
+                                                                   int nfeat,
+                                                                   double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nw = blockDim.x / 64;
+  const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const int el = lane >> 3, s = lane & 7;
+  const int F = C * nfeat;
+  double* xch = smem + w * 64 * kSlot;
+  double* feat = smem + nw * 64 * kSlot;  // [8][F]
+  double* norm = feat + 8 * F;            // [8]
+  const int64_t e0 = (int64_t)blockIdx.x * 8;
+  const int64_t e = e0 + el;
+  const bool valid = e < n;
+  for (int c = w; c < C; c += nw) {
+    double x[kIn];
+    const double* src = ep + (valid ? (e * C + c) * kPost + skip : 0);
+#pragma unroll
+    for (int k = 0; k < kIn; ++k) x[k] = valid ? src[(kSegLen * s + k) & (kWin - 1)] : 0.0;
+    double a6, d6;
+    dwt8_cascade<FAST>(x, xch, lane & ~7, s, a6, d6);
+    if (valid) {
+      if (s < nfeat) feat[el * F + c * nfeat + s] = a6;
+      if (8 + s < nfeat) feat[el * F + c * nfeat + 8 + s] = d6;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    double acc = 0.0;
+    for (int i = 0; i < F; ++i) {
+      const double f = feat[threadIdx.x * F + i];
+      acc = acc + f * f;  // Math.pow(f, 2) summed in index order
+    }
+    norm[threadIdx.x] = sqrt(acc);
+  }
+  __syncthreads();
+  const int64_t ne = (n - e0) < 8 ? (n - e0) : 8;
+  for (int idx = threadIdx.x; idx < ne * F; idx += blockDim.x)
+    out[e0 * F + idx] = feat[idx] / norm[idx / F];
+}
+
+// ---- synthetic recordings ------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float unit_noise(uint64_t seed, uint64_t key) {  // [-1, 1)
+  return (float)(splitmix64(seed ^ splitmix64(key)) >> 40) * (2.0f / 16777216.0f) - 1.0f;
+}
+
+// DC -25000 counts, a bounded random walk (piecewise-linear between random knots every 64 and
+// 1024 frames), a 10 Hz sinusoid of 200 counts and white noise, clipped to int16; about one
+// sample in 65536 is a -32768 saturation.
+__global__ __launch_bounds__(256) void synth_kernel(int16_t* __restrict__ dst, int64_t n_frames,
+                                                    int ct, uint64_t seed) {
+  const int64_t total = n_frames * ct;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = idx / ct;
+    const int c = (int)(idx - t * ct);
+    const uint64_t ck = (uint64_t)c << 48;
+    const int64_t k1 = t >> 6, k2 = t >> 10;
+    const float f1 = (float)(t & 63) * (1.0f / 64.0f), f2 = (float)(t & 1023) * (1.0f / 1024.0f);
+    const float w1 = unit_noise(seed, ck | (uint64_t)(2 * k1)) * (1.0f - f1) +
+                     unit_noise(seed, ck | (uint64_t)(2 * k1 + 2)) * f1;
+    const float w2 = unit_noise(seed + 1, ck | (uint64_t)k2) * (1.0f - f2) +
+                     unit_noise(seed + 1, ck | (uint64_t)(k2 + 1)) * f2;
+    const float sine = 200.0f * __sinf(6.2831853f * 10.0f * (float)(t % 1000) / 1000.0f + (float)c);
+    const float noise = 40.0f * unit_noise(seed + 2, (uint64_t)idx);
+    float v = -25000.0f + 1500.0f * w1 + 4000.0f * w2 + sine + noise;
+    if (unit_noise(seed + 3, (uint64_t)idx) < -0.99997f) v = -40000.0f;
+    v = fminf(fmaxf(v, -32768.0f), 32767.0f);
+    dst[idx] = (int16_t)__float2int_rn(v);
+  }
+}
+
+}  // namespace dev
+
+// ---- launchers ---------------------------------------------------------------------------------
+hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                             const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                             double* out) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((unsigned)n), block(256);
+  if (fmt == 0)
+    hipLaunchKernelGGL(dev::cut_epochs_kernel<int16_t>, grid, block, 0, st,
+                       (const int16_t*)raw, n_frames, ct, sel, C, pos, out);
+  else
+    hipLaunchKernelGGL(dev::cut_epochs_kernel<float>, grid, block, 0, st, (const float*)raw,
+                       n_frames, ct, sel, C, pos, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
+                                       int nfeat, bool fast, double* out) {
+  if (n == 0) return hipSuccess;
+  const int nw = C < 4 ? C : 4;
+  const size_t smem = sizeof(double) * ((size_t)nw * 64 * dev::kSlot + 8 * (size_t)C * nfeat + 8);
+  dim3 grid((unsigned)((n + 7) / 8)), block(64 * nw);
+  if (fast)
+    hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
+                       skip, nfeat, out);
+  else
+    hipLaunchKernelGGL(dev::features_from_epochs_kernel<false>, grid, block, smem, st, ep, n, C,
+                       skip, nfeat, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed) {
+  const int64_t total = n_frames * ct;
+  if (total == 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(dev::synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst, n_frames,
+                     ct, seed);
+  return hipGetLastError();
+}
+
+}  // namespace eegfx

@@ -1,0 +1,201 @@
+/*
+ * eegfx.h -- C ABI of the MI355X-native epoch-to-feature path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (NEUROINFORMATICS-GROUP-FAV-KIV-ZCU/EEG_DataAnalysisPackage, paths relative to its checkout):
+ *
+ *   src/main/java/cz/zcu/kiv/DataTransformation/OffLineDataProvider.java   (processEEGFiles)
+ *   src/main/java/cz/zcu/kiv/FeatureExtraction/IFeatureExtraction.java     (extractFeatures)
+ *   src/main/java/cz/zcu/kiv/FeatureExtraction/WaveletTransform.java       (fe=dwt-8)
+ *
+ * Every entry point below names the reference interface it replaces.  The ABI is plain C:
+ * no C++ or torch types, caller-owned buffers, int status returns (0 = ok, < 0 = error),
+ * error text from eegfx_last_error() (thread-local).  Java binds it through JNI
+ * (INTEGRATION.md); Python binds it through ctypes (eeg_dataanalysispackage_amd/_lib.py).
+ *
+ * Threading: every function is reentrant.  Calls that take an eegfx_ctx serialise on that
+ * context's HIP stream; use one context per calling thread (e.g. per Spark executor thread,
+ * LogisticRegressionClassifier.java:50,90) for concurrency.
+ *
+ * Memory: pointer arguments of compute calls are host or device pointers as selected by the
+ * `mem` argument (EEGFX_MEM_HOST: the library stages through its own device buffers and
+ * returns after the results are back in host memory; EEGFX_MEM_DEVICE: pointers are HIP
+ * device pointers, the work is enqueued on the context stream and the call returns without
+ * synchronising -- call eegfx_ctx_synchronize()).
+ */
+#ifndef EEGFX_H_
+#define EEGFX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EEGFX_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define EEGFX_OK 0
+#define EEGFX_EINVAL -1    /* bad argument: IllegalArgumentException in the reference      */
+#define EEGFX_EIO -2       /* file missing / unreadable: IOException                       */
+#define EEGFX_EFORMAT -3   /* malformed .vhdr/.vmrk/info.txt: NumberFormatException & co.  */
+#define EEGFX_EHIP -4      /* HIP runtime error                                            */
+#define EEGFX_ENOMEM -5    /* allocation failure                                           */
+#define EEGFX_ERANGE -6    /* epoch out of range: ArrayIndexOutOfBoundsException           */
+#define EEGFX_ENOTSUP -7   /* parameter combination without a kernel                       */
+
+/* ---- constants of the reference (Utils/Const.java:61-71, WaveletTransform.java:47-87) ---- */
+#define EEGFX_PRESTIMULUS 100   /* Const.PREESTIMULUS_VALUES  */
+#define EEGFX_POSTSTIMULUS 750  /* Const.POSTSTIMULUS_VALUES  */
+#define EEGFX_USED_CHANNELS 3   /* Const.USED_CHANNELS        */
+#define EEGFX_DWT8_NAME 8       /* fe=dwt-8: WaveletTransform(8, 512, 175, 16), PipelineBuilder.java:131 */
+#define EEGFX_DWT8_EPOCH_SIZE 512
+#define EEGFX_DWT8_SKIP 175
+#define EEGFX_DWT8_FEATURE_SIZE 16
+
+/* sample formats of BrainVision BinaryFormat= */
+#define EEGFX_INT_16 0
+#define EEGFX_IEEE_FLOAT_32 1
+
+#define EEGFX_MEM_HOST 0
+#define EEGFX_MEM_DEVICE 1
+
+/* numerics of the DWT filter bank */
+#define EEGFX_EXACT 0   /* separate fp64 mul + add in the reference order: bit-exact to Java */
+#define EEGFX_FMA 1     /* fp64 fused multiply-add: within 1e-9 relative, fewer instructions  */
+
+typedef struct eegfx_ctx eegfx_ctx;
+typedef struct eegfx_odp eegfx_odp;
+
+/* ---- library / context ------------------------------------------------------------------ */
+const char* eegfx_version(void);
+const char* eegfx_last_error(void);
+int eegfx_device_count(int* count);
+/* Creates a context on HIP device `device` with its own non-blocking stream. */
+int eegfx_ctx_create(int device, eegfx_ctx** out);
+/* Makes the context enqueue on `hip_stream` (hipStream_t, e.g. torch's current stream);
+ * NULL restores the context's own stream. */
+int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream);
+int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | EEGFX_FMA */
+int eegfx_ctx_synchronize(eegfx_ctx* ctx);
+/* Time of the last kernel launched by this context, measured with HIP events on its stream
+ * (ms; valid after eegfx_ctx_synchronize).  Used by bench.py for the roofline leg. */
+int eegfx_ctx_last_kernel_ms(eegfx_ctx* ctx, float* ms);
+int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable);
+int eegfx_ctx_destroy(eegfx_ctx* ctx);
+
+/* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */
+typedef struct {
+  int32_t number;        /* 1-based channel number (Ch<n>=)            ChannelInfo.getNumber() */
+  char name[64];         /* first field, "\1" decoded to ','           ChannelInfo.getName()   */
+  char reference[64];
+  double resolution;     /* third field; 1.0 when empty                                        */
+  char unit[32];         /*                                            ChannelInfo.getUnits()  */
+} eegfx_channel_info;
+
+typedef struct {
+  int32_t n_channels;          /* NumberOfChannels=                                           */
+  int32_t binary_format;       /* EEGFX_INT_16 | EEGFX_IEEE_FLOAT_32                           */
+  int32_t multiplexed;         /* DataOrientation=MULTIPLEXED -> 1, VECTORIZED -> 0           */
+  double sampling_interval_us; /* SamplingInterval=                                           */
+  char data_file[512];
+  char marker_file[512];
+} eegfx_header_info;
+
+typedef struct {
+  int32_t number;         /* Mk<n>                                                           */
+  char type[64];          /* e.g. "Stimulus", "New Segment"                                  */
+  char description[64];   /* e.g. "S  2"                       EEGMarker.getStimulus()       */
+  int64_t position;       /* data point, used verbatim as a 0-based index                    */
+  int64_t size;
+  int32_t channel;
+  int32_t stimulus_index; /* int(digits(description)) - 1, or -1 (OffLineDataProvider.java:207-214) */
+} eegfx_marker;
+
+/* DataTransformer.getChannelInfo(vhdr) (OffLineDataProvider.java:167-168). `channels` may be
+ * NULL to query; at most max_channels entries are written. */
+int eegfx_read_header(const char* vhdr_path, eegfx_header_info* info,
+                      eegfx_channel_info* channels, int32_t max_channels);
+/* DataTransformer.readMarkerList(vmrk) (OffLineDataProvider.java:196). `markers` may be NULL
+ * to query the count. */
+int eegfx_read_markers(const char* vmrk_path, eegfx_marker* markers, int64_t max_markers,
+                       int64_t* n_markers);
+/* Number of frames of a .eeg file given its header (file size / (channels * sample size)). */
+int eegfx_recording_frames(const char* vhdr_path, const char* eeg_path, int64_t* n_frames);
+/* Reads the raw multiplexed samples of a .eeg file into `dst` (n_frames * n_channels samples of
+ * the header's binary format; host or device memory per `mem`).  The decode itself (a3) is done
+ * by the kernels, fused with the epoch cut. */
+int eegfx_read_raw(eegfx_ctx* ctx, const char* vhdr_path, const char* eeg_path, void* dst,
+                   int64_t capacity_bytes, int mem);
+
+/* ---- marker planning: OffLineDataProvider.java:200-265 (a4 + a8) ----------------------------
+ * For each marker in order: skip it (no state change) iff position-100 < 0 or
+ * position-100 > n_frames (the AIOOBE of Arrays.copyOfRange, :220-225, caught at :262-264);
+ * target iff stimulus_index+1 == guessed (:238-240); class balance (:248-260) with
+ * *balance = numberOfTargets - numberOfNonTargets carried across files: accept a target iff
+ * *balance <= 0, a non-target iff *balance >= 0.  Writes the accepted positions and labels
+ * (1.0 / 0.0) in order.  pos_out/label_out may be NULL to count. */
+int eegfx_plan_markers(const eegfx_marker* markers, int64_t n_markers, int64_t n_frames,
+                       int32_t guessed, int64_t* balance, int64_t* pos_out, double* label_out,
+                       int64_t* n_selected);
+
+/* ---- compute ------------------------------------------------------------------------------ */
+/* a3 + a5..a7: raw multiplexed recording -> baseline-corrected epochs double[n][C][750]
+ * (OffLineDataProvider.java:216-233 + EpochHolder.setFZ/CZ/PZ, the List<double[][]> that
+ * getData() returns).  cols[c] = 0-based column of selected channel c, res[c] its resolution
+ * (host arrays, C <= 64).  raw/pos/epochs_out per `mem`. */
+int eegfx_cut_epochs_f64(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                         int32_t n_channels_total, const int32_t* cols, const float* res,
+                         int32_t C, const int64_t* pos, int64_t n_epochs, double* epochs_out,
+                         int mem);
+
+/* IFeatureExtraction.extractFeatures (IFeatureExtraction.java:27-35), batched over n epochs:
+ * WaveletTransform(name, epoch_size, skip, feature_size).extractFeatures for each
+ * epochs[i] = double[C][750] (WaveletTransform.java:107-141).  out = double[n][C*feature_size],
+ * each row L2-normalised (SignalProcessing.java:38-52).  Supported: name 8 with epoch_size 512,
+ * skip + 512 <= 750 and feature_size <= 16 (the coefficients a6 ++ d6), C <= 64. */
+int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, int32_t C,
+                               int32_t name, int32_t epoch_size, int32_t skip,
+                               int32_t feature_size, double* out, int mem);
+
+/* The fused hot path: raw multiplexed recording -> dwt-8 feature matrix, without materialising
+ * the epochs.  Equals eegfx_cut_epochs_f64 followed by eegfx_extract_features_f64 with
+ * (8, 512, 175, 16), bit for bit under EEGFX_EXACT. */
+int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                            int32_t n_channels_total, const int32_t* cols, const float* res,
+                            int32_t C, const int64_t* pos, int64_t n_epochs, double* features,
+                            int mem);
+
+/* Deterministic synthetic multiplexed int16 recording, generated on device:
+ * DC -25000 counts + bounded random walk + 10 Hz sinusoid, clipped to int16.  dst is a device
+ * pointer of n_frames * n_channels int16. */
+int eegfx_synth_recording(eegfx_ctx* ctx, int16_t* dst, int64_t n_frames, int32_t n_channels,
+                          uint64_t seed);
+
+/* ---- OffLineDataProvider (OffLineDataProvider.java:42-380) ----------------------------------
+ * Same argument conventions as the Java constructor: args = { "<info.txt>" } or
+ * { "<file.eeg>", "<guessed>", optional... } (1..6 entries).  Paths are local files (the HDFS
+ * client of the reference is out of scope).  load_data never fails: like the reference
+ * (:88-98) it stops at the first fatal error and keeps what was loaded; the message is
+ * available from eegfx_odp_error(). */
+/* ctx may be NULL: a planning-only provider parses, selects and labels (positions, labels,
+ * file indices) without reading the sample payload or touching a GPU. */
+int eegfx_odp_create(eegfx_ctx* ctx, const char* const* args, int32_t n_args, eegfx_odp** out);
+int eegfx_odp_load_data(eegfx_odp* odp);
+const char* eegfx_odp_error(const eegfx_odp* odp);       /* "" when loading succeeded */
+int64_t eegfx_odp_num_epochs(const eegfx_odp* odp);
+/* getData(): double[n][3][750] host copy */
+int eegfx_odp_get_data(const eegfx_odp* odp, double* out);
+/* getDataLabels(): double[n] */
+int eegfx_odp_get_labels(const eegfx_odp* odp, double* out);
+/* Selected marker positions (int64[n]) and source file index (int32[n]) of every epoch. */
+int eegfx_odp_get_positions(const eegfx_odp* odp, int64_t* pos_out, int32_t* file_out);
+/* fe=dwt-8 features of every loaded epoch, computed on the device from the resident epochs. */
+int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int32_t skip,
+                           int32_t feature_size, double* out);
+void eegfx_odp_destroy(eegfx_odp* odp);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EEGFX_H_ */
