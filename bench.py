@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
     ap.add_argument("--numerics", choices=["exact", "fma"], default="exact")
-    ap.add_argument("--cpu-sample", type=int, default=100_000,
+    ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather leg")
@@ -86,8 +86,11 @@ def main():
     n = args.epochs
     n_frames = FRAMES_PER_EPOCH * n + 2000
     ctx = fx.Context(local, numerics=args.numerics)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)  # kernels run on torch's stream: events see them
+    # A dedicated (non-null) torch stream shared with the context: the kernels run on it, so the
+    # HIP events recorded on it bracket exactly the launches of the timed region.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
 
     raw = torch.empty((n_frames, 3), dtype=torch.int16, device=dev)
     ctx.synth_recording(raw, 3, SEED + rank)

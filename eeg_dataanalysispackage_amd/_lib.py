@@ -108,6 +108,14 @@ def lib() -> ctypes.CDLL:
     """Loads libeegfx.so once (raises if it is missing -- no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 and
+        # libhsa-runtime64.so.  Loading torch first makes libeegfx's libamdhip64.so.7 dependency
+        # resolve (by SONAME) to that same runtime, so torch tensors and eegfx contexts share one
+        # device context.  Without torch, the ROCm runtime under /opt/rocm is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                               "(make -C eeg_dataanalysispackage_amd/csrc)")

@@ -96,7 +96,7 @@ struct eegfx_ctx {
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_time = false;
-  DevBuf raw, pos, out, scratch;
+  DevBuf raw, pos, out, scratch, fused;
 
   void activate() const { HIP_CHECK(hipSetDevice(device)); }
   void tic() {
@@ -130,7 +130,9 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
                            double* out) {
   const bool fast = ctx->numerics == EEGFX_FMA;
   ctx->tic();
-  hipError_t e = launch_fused_features(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast, out);
+  void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
+  hipError_t e =
+      launch_fused_features(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast, fscratch, out);
   if (e == hipErrorNotSupported) {
     (void)hipGetLastError();
     double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
@@ -440,6 +442,7 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     ctx->pos.release();
     ctx->out.release();
     ctx->scratch.release();
+    ctx->fused.release();
     (void)hipEventDestroy(ctx->ev0);
     (void)hipEventDestroy(ctx->ev1);
     (void)hipStreamDestroy(ctx->own);

@@ -104,27 +104,45 @@ __device__ __forceinline__ void halo_exchange(double* v, double* xch, int gbase,
   wave_sync();
 }
 
+// Same contract as halo_exchange, through the cross-lane network (ds_bpermute) instead of an
+// LDS slot: no LDS allocation and no ordering fences.
+template <int CNT>
+__device__ __forceinline__ void halo_shuffle(double* v, int gbase, int s) {
+  constexpr int P = CNT < 8 ? CNT : 8;
+  double h[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) h[m] = __shfl(v[m % P], gbase + ((s + 1 + m / P) & 7), 64);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) v[CNT + m] = h[m];
+}
+
+template <int CNT, bool SHFL>
+__device__ __forceinline__ void halo(double* v, double* xch, int gbase, int s) {
+  if constexpr (SHFL) halo_shuffle<CNT>(v, gbase, s);
+  else halo_exchange<CNT>(v, xch, gbase, s);
+}
+
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
 // xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
 // Returns a6[s] and d6[s].
-template <bool FAST>
+template <bool FAST, bool SHFL = false>
 __device__ __forceinline__ void dwt8_cascade(const double (&x)[kIn], double* xch, int gbase, int s,
                                              double& a6, double& d6) {
   double a1[32 + 8];
   lowpass<32, FAST>(x, a1);
-  halo_exchange<32>(a1, xch, gbase, s);
+  halo<32, SHFL>(a1, xch, gbase, s);
   double a2[16 + 8];
   lowpass<16, FAST>(a1, a2);
-  halo_exchange<16>(a2, xch, gbase, s);
+  halo<16, SHFL>(a2, xch, gbase, s);
   double a3[8 + 8];
   lowpass<8, FAST>(a2, a3);
-  halo_exchange<8>(a3, xch, gbase, s);
+  halo<8, SHFL>(a3, xch, gbase, s);
   double a4[4 + 8];
   lowpass<4, FAST>(a3, a4);
-  halo_exchange<4>(a4, xch, gbase, s);
+  halo<4, SHFL>(a4, xch, gbase, s);
   double a5[2 + 8];
   lowpass<2, FAST>(a4, a5);
-  halo_exchange<2>(a5, xch, gbase, s);
+  halo<2, SHFL>(a5, xch, gbase, s);
   a6 = fir10<FAST, false>(a5);
   d6 = fir10<FAST, true>(a5);
 }
