@@ -9,9 +9,10 @@ recording of the same shape (weak scaling: epochs are independent, no data-path 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--numerics exact|fma]
 
 Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").  Extra legs:
-  roofline      algorithmic bytes per launch / average launch duration, measured with HIP
-                events on the stream the kernel runs on, against 8.0 TB/s (MI355X_MICROARCH.md);
-                traffic from the committed rocprofv3 PMC summary when one matches (else null);
+  roofline      the dominant kernel (window_kernel): its algorithmic bytes per launch / its
+                average launch duration, measured with HIP events that the context records on
+                the stream the kernel runs on, against 8.0 TB/s (MI355X_MICROARCH.md); traffic =
+                HBM bytes per launch from the committed rocprofv3 PMC summary (else null);
   cpu_baseline  the C restatement (oracle/, reference-faithful full pyramid) timed on the host
                 cores on a bounded sample of the same workload (rank 0, N=1 only).
 """
@@ -27,7 +28,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "epochs/sec feature-extracted (whole node) + % HBM roofline, 1/2/4/8 GPUs"
-BYTES_PER_EPOCH = 612 * 3 * 2 + 8 + 48 * 8   # 3,672 in + 8 marker + 384 out
+BYTES_PER_EPOCH = 612 * 3 * 2 + 8 + 48 * 8   # whole path: 3,672 in + 8 marker + 384 out (8d)
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
@@ -39,7 +40,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
-    ap.add_argument("--numerics", choices=["exact", "fma"], default="exact")
+    ap.add_argument("--numerics", choices=["exact", "fma"], default="fma",
+                    help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
+                         "exact: the reference's operation order, bit-identical")
+    ap.add_argument("--alt-steps", type=int, default=10,
+                    help="steps of a second, untimed-for-value pass in the other numerics mode "
+                         "(reported under 'alt_numerics'; 0 disables)")
     ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
@@ -111,6 +117,7 @@ def main():
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    ctx.set_timing(True)  # HIP events around each window_kernel launch, on the context stream
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
@@ -121,12 +128,38 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # average launch duration on its stream
+    step_ms = ev0.elapsed_time(ev1) / args.steps      # both kernels, device clock
+    launches, win_total_ms, win_bytes = ctx.kernel_stats()
+    ctx.set_timing(False)
+    if launches != args.steps:
+        raise RuntimeError(f"timed {launches} window_kernel launches for {args.steps} steps")
+    kernel_ms = win_total_ms / launches                 # average window_kernel launch duration
+    kernel_bytes = win_bytes // launches                # algorithmic bytes per launch
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+    elapsed, kernel_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
+
+    # the other numerics mode, same buffers (reported beside the headline, not as value)
+    alt = None
+    if args.alt_steps > 0:
+        other = "exact" if args.numerics == "fma" else "fma"
+        ctx.set_numerics(other)
+        step()
+        torch.cuda.synchronize(dev)
+        a0 = time.perf_counter()
+        for _ in range(args.alt_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        at = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device=dev)
+        if distributed:
+            dist.all_reduce(at, op=dist.ReduceOp.MAX)
+        alt = {"numerics": other, "value": round(world * n * args.alt_steps / float(at[0]), 1),
+               "ms_per_step": round(float(at[0]) / args.alt_steps * 1e3, 4)}
+        ctx.set_numerics(args.numerics)
+        step()  # leave `out` in the headline mode for the checks below
+        torch.cuda.synchronize(dev)
 
     # sanity of the produced features (unit rows) -- outside the timed region
     norms = torch.linalg.vector_norm(out, dim=1)
@@ -135,12 +168,12 @@ def main():
     gather = None
     if distributed and not args.no_gather:
         # RCCL over xGMI only moves the feature matrices: all-gather into rank order.
-        full = torch.empty((world * n, 48), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(full, out)  # warm
+        from eeg_dataanalysispackage_amd.sharding import gather_features
+        full = gather_features(out, world * n)  # warm
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(full, out)
+        full = gather_features(out, world * n)
         torch.cuda.synchronize(dev)
         gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
@@ -155,8 +188,8 @@ def main():
     if rank == 0:
         workload_key = f"fused_dwt8_c3_int16_{n}_{args.numerics}"
         value = world * n * args.steps / elapsed
-        launch_bytes = n * BYTES_PER_EPOCH
-        achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9
+        path_gbs = n * BYTES_PER_EPOCH / (step_ms * 1e-3) / 1e9
         prof = traffic_from_profiles(workload_key)
         line = {
             "metric": METRIC,
@@ -177,7 +210,7 @@ def main():
                 "epochs_per_gpu": n,
                 "channels": 3,
                 "numerics": args.numerics,
-                "kernel": "fused_features_kernel<3,3>",
+                "kernels": ["baseline_kernel<int16,3>", "window_kernel<int16,3>"],
                 "unit_rows_check": ok_norm,
             },
             "roofline": {
@@ -187,11 +220,19 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": (round(prof["hbm_bytes_per_launch"]) if prof else None),
+                "kernel": "window_kernel<int16,3>",
                 "kernel_ms": round(kernel_ms, 4),
-                "bytes_per_epoch": BYTES_PER_EPOCH,
+                "bytes_per_launch": kernel_bytes,
+                "bytes_per_epoch": kernel_bytes // n,
+                "traffic_source": (prof.get("source") if prof else None),
+                "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": BYTES_PER_EPOCH,
+                               "GBps": round(path_gbs, 1),
+                               "frac": round(path_gbs / HBM_PEAK_GBS, 4)},
             },
             "cpu_baseline": cpu,
         }
+        if alt:
+            line["alt_numerics"] = alt
         if gather:
             line["gather"] = gather
         print(json.dumps(line), flush=True)

@@ -74,7 +74,8 @@ SIGNATURES = {
     "eegfx_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
     "eegfx_ctx_set_numerics": (c_int, [c_void_p, c_int]),
     "eegfx_ctx_synchronize": (c_int, [c_void_p]),
-    "eegfx_ctx_last_kernel_ms": (c_int, [c_void_p, POINTER(c_float)]),
+    "eegfx_ctx_kernel_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double),
+                                       POINTER(c_int64)]),
     "eegfx_ctx_set_timing": (c_int, [c_void_p, c_int]),
     "eegfx_ctx_destroy": (c_int, [c_void_p]),
     "eegfx_read_header": (c_int, [c_char_p, POINTER(HeaderInfo), POINTER(ChannelInfo), c_int32]),

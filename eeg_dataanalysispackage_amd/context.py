@@ -7,7 +7,7 @@ enqueued on the context stream and the call returns without synchronising).
 from __future__ import annotations
 
 import ctypes
-from ctypes import c_float, c_int, c_int64, c_void_p
+from ctypes import c_int, c_int64, c_void_p
 from typing import Optional, Sequence
 
 import numpy as np
@@ -67,10 +67,13 @@ class Context:
     def synchronize(self) -> None:
         check(lib().eegfx_ctx_synchronize(self.handle))
 
-    def last_kernel_ms(self) -> float:
-        ms = c_float()
-        check(lib().eegfx_ctx_last_kernel_ms(self.handle, ctypes.byref(ms)))
-        return float(ms.value)
+    def kernel_stats(self):
+        """(timed launches, summed duration in ms, algorithmic bytes) of the dominant kernel
+        since timing was (re)enabled -- HIP events on the context stream."""
+        n, ms, by = c_int64(), ctypes.c_double(), c_int64()
+        check(lib().eegfx_ctx_kernel_stats(self.handle, ctypes.byref(n), ctypes.byref(ms),
+                                           ctypes.byref(by)))
+        return int(n.value), float(ms.value), int(by.value)
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

@@ -94,19 +94,39 @@ struct eegfx_ctx {
   hipStream_t stream = nullptr;
   int numerics = EEGFX_EXACT;
   bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool have_time = false;
+  // HIP event pairs bracketing each timed (dominant) kernel launch on the context stream, plus
+  // the algorithmic bytes each launch moved; summed by eegfx_ctx_kernel_stats.
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  std::vector<int64_t> event_bytes;
+  size_t n_timed = 0;
   DevBuf raw, pos, out, scratch, fused;
 
   void activate() const { HIP_CHECK(hipSetDevice(device)); }
   void tic() {
-    if (timing) HIP_CHECK(hipEventRecord(ev0, stream));
-  }
-  void toc() {
-    if (timing) {
-      HIP_CHECK(hipEventRecord(ev1, stream));
-      have_time = true;
+    if (!timing) return;
+    if (n_timed == events.size()) {
+      hipEvent_t a, b;
+      HIP_CHECK(hipEventCreate(&a));
+      HIP_CHECK(hipEventCreate(&b));
+      events.emplace_back(a, b);
+      event_bytes.push_back(0);
     }
+    HIP_CHECK(hipEventRecord(events[n_timed].first, stream));
+  }
+  void toc(int64_t bytes) {
+    if (!timing) return;
+    HIP_CHECK(hipEventRecord(events[n_timed].second, stream));
+    event_bytes[n_timed] = bytes;
+    ++n_timed;
+  }
+  void destroy_events() {
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    events.clear();
+    event_bytes.clear();
+    n_timed = 0;
   }
 };
 
@@ -129,19 +149,21 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
                            const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                            double* out) {
   const bool fast = ctx->numerics == EEGFX_FMA;
-  ctx->tic();
-  void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
-  hipError_t e =
-      launch_fused_features(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast, fscratch, out);
-  if (e == hipErrorNotSupported) {
-    (void)hipGetLastError();
-    double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
-    HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep));
-    e = launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
-                                    EEGFX_DWT8_FEATURE_SIZE, fast, out);
+  if (fused_supported(fmt, ct, C, out)) {
+    void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
+    HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch));
+    ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
+    HIP_CHECK(launch_fused_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fast, fscratch,
+                                  out));
+    ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
+    return;
   }
-  HIP_CHECK(e);
-  ctx->toc();
+  double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
+  ctx->tic();
+  HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep));
+  HIP_CHECK(launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
+                                        EEGFX_DWT8_FEATURE_SIZE, fast, out));
+  ctx->toc(0);
 }
 
 }  // namespace
@@ -387,8 +409,6 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     c->activate();
     HIP_CHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->stream = c->own;
-    HIP_CHECK(hipEventCreate(&c->ev0));
-    HIP_CHECK(hipEventCreate(&c->ev1));
     *out = c.release();
   });
 }
@@ -411,8 +431,10 @@ int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics) {
 int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable) {
   return guarded([&] {
     if (!ctx) fail(EEGFX_EINVAL, "null context");
+    ctx->activate();
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
     ctx->timing = enable != 0;
-    ctx->have_time = false;
+    ctx->n_timed = 0;  // events are reused
   });
 }
 
@@ -424,12 +446,22 @@ int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
   });
 }
 
-int eegfx_ctx_last_kernel_ms(eegfx_ctx* ctx, float* ms) {
+int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,
+                           int64_t* total_bytes) {
   return guarded([&] {
-    if (!ctx || !ms) fail(EEGFX_EINVAL, "null argument");
-    if (!ctx->have_time) fail(EEGFX_EINVAL, "no timed launch (enable eegfx_ctx_set_timing)");
-    HIP_CHECK(hipEventSynchronize(ctx->ev1));
-    HIP_CHECK(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    if (!ctx || !launches || !total_ms || !total_bytes) fail(EEGFX_EINVAL, "null argument");
+    double ms = 0.0;
+    int64_t bytes = 0;
+    for (size_t i = 0; i < ctx->n_timed; ++i) {
+      float t = 0.0f;
+      HIP_CHECK(hipEventSynchronize(ctx->events[i].second));
+      HIP_CHECK(hipEventElapsedTime(&t, ctx->events[i].first, ctx->events[i].second));
+      ms += t;
+      bytes += ctx->event_bytes[i];
+    }
+    *launches = (int64_t)ctx->n_timed;
+    *total_ms = ms;
+    *total_bytes = bytes;
   });
 }
 
@@ -443,8 +475,7 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     ctx->out.release();
     ctx->scratch.release();
     ctx->fused.release();
-    (void)hipEventDestroy(ctx->ev0);
-    (void)hipEventDestroy(ctx->ev1);
+    ctx->destroy_events();
     (void)hipStreamDestroy(ctx->own);
     delete ctx;
   });
@@ -493,7 +524,7 @@ int eegfx_cut_epochs_f64(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n
     double* d_out = mem == EEGFX_MEM_DEVICE ? epochs_out : (double*)ctx->out.get(out_bytes);
     ctx->tic();
     HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out));
-    ctx->toc();
+    ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(epochs_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -519,7 +550,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
     ctx->tic();
     HIP_CHECK(launch_features_from_epochs(ctx->stream, d_in, n, C, skip, feature_size,
                                           ctx->numerics == EEGFX_FMA, d_out));
-    ctx->toc();
+    ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       HIP_CHECK(hipStreamSynchronize(ctx->stream));

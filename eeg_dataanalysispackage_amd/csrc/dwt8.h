@@ -122,6 +122,33 @@ __device__ __forceinline__ void halo(double* v, double* xch, int gbase, int s) {
   else halo_exchange<CNT>(v, xch, gbase, s);
 }
 
+// The cascade in two parts, so a caller can issue memory traffic between level 1 (which consumes
+// the 72 decoded samples) and levels 2..6 (which only need the 40-value level-1 slice).
+template <bool FAST, bool SHFL = false>
+__device__ __forceinline__ void dwt8_level1(const double (&x)[kIn], double* xch, int gbase, int s,
+                                            double (&a1)[40]) {
+  lowpass<32, FAST>(x, a1);
+  halo<32, SHFL>(a1, xch, gbase, s);
+}
+template <bool FAST, bool SHFL = false>
+__device__ __forceinline__ void dwt8_levels2to6(double (&a1)[40], double* xch, int gbase, int s,
+                                                double& a6, double& d6) {
+  double a2[16 + 8];
+  lowpass<16, FAST>(a1, a2);
+  halo<16, SHFL>(a2, xch, gbase, s);
+  double a3[8 + 8];
+  lowpass<8, FAST>(a2, a3);
+  halo<8, SHFL>(a3, xch, gbase, s);
+  double a4[4 + 8];
+  lowpass<4, FAST>(a3, a4);
+  halo<4, SHFL>(a4, xch, gbase, s);
+  double a5[2 + 8];
+  lowpass<2, FAST>(a4, a5);
+  halo<2, SHFL>(a5, xch, gbase, s);
+  a6 = fir10<FAST, false>(a5);
+  d6 = fir10<FAST, true>(a5);
+}
+
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
 // xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
 // Returns a6[s] and d6[s].

@@ -22,13 +22,20 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
                                        int nfeat, bool fast, double* out);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
-// Fused raw -> features (baseline_kernel + window_kernel, fused.hip).  `scratch` holds
-// fused_scratch_bytes(n, C) bytes of device memory (the per-epoch baselines).  Returns
-// hipErrorNotSupported (without launching) when no fused kernel covers (fmt, ct, C); the caller
-// then runs cut + features through a device scratch buffer.
+// Fused raw -> features (fused.hip): baseline_kernel then window_kernel.  `scratch` holds
+// fused_scratch_bytes(n, C) bytes of device memory (the per-epoch baselines).  fused_supported
+// says whether a fused kernel covers (fmt, ct, C); otherwise the caller runs cut + features
+// through a device scratch buffer.
+bool fused_supported(int fmt, int ct, int C, const double* out);
 size_t fused_scratch_bytes(int64_t n, int C);
-hipError_t launch_fused_features(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 bool fast, void* scratch, double* out);
+                                 void* scratch);
+hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
+                               const void* scratch, double* out);
+// Algorithmic HBM bytes per epoch of window_kernel (the dominant kernel): window frames, the
+// baseline and marker position it reads, the feature row it writes.
+int64_t fused_window_bytes_per_epoch(int ct, int C);
 
 }  // namespace eegfx

@@ -78,10 +78,13 @@ int eegfx_ctx_create(int device, eegfx_ctx** out);
 int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream);
 int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | EEGFX_FMA */
 int eegfx_ctx_synchronize(eegfx_ctx* ctx);
-/* Time of the last kernel launched by this context, measured with HIP events on its stream
- * (ms; valid after eegfx_ctx_synchronize).  Used by bench.py for the roofline leg. */
-int eegfx_ctx_last_kernel_ms(eegfx_ctx* ctx, float* ms);
+/* Kernel timing for the roofline leg of bench.py.  While enabled, every compute call brackets its
+ * dominant kernel (window_kernel for the fused path) with a pair of HIP events on the context
+ * stream; eegfx_ctx_kernel_stats returns the number of timed launches, their summed duration
+ * (ms) and the algorithmic HBM bytes they moved.  Enabling (again) resets the counters. */
 int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable);
+int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,
+                           int64_t* total_bytes);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
 /* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */

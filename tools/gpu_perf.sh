@@ -17,13 +17,15 @@ for ABL in ${ABLS:-0 1 2 3 4}; do
 done
 [ "${PMC:-1}" = "1" ] || exit 0
 cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --cpu-sample 0 > "$OUT/trace.log" 2>&1 || { tail -20 "$OUT/trace.log"; exit 1; }
+grep -E "window|baseline" "$OUT"/trace/run_kernel_stats.csv | cut -c1-160
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 i=0
 while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i+1))
   echo "== pmc pass $i: $GROUP"
-  timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex window --output-format csv -d "$OUT/pmc$i" -o run -- python3 $ROOT/bench.py --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/pmc$i.log" 2>&1 || { tail -20 "$OUT/pmc$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex "${PMC_REGEX:-window}" --output-format csv -d "$OUT/pmc$i" -o run -- python3 $ROOT/bench.py --steps 5 --warmup 1 --cpu-sample 0 > "$OUT/pmc$i.log" 2>&1 || { tail -20 "$OUT/pmc$i.log"; exit 1; }
 done <<'GROUPS'
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS

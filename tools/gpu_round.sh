@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round evidence on one GPU box: parity tests -> smoke -> bench (fma headline, exact alt) ->
+# rocprofv3 kernel trace + stats of the bench -> PMC FETCH_SIZE / WRITE_SIZE passes on
+# window_kernel (one counter per pass, kernel trace only) -> traffic summaries.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+TAG=${TAG:-round}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+if [ "${TESTS:-1}" = "1" ]; then
+  echo "== pytest -m gpu"; date
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+  tail -3 "$OUT/pytest_gpu.log"
+  echo "== smoke"; date
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
+  cat "$OUT/smoke.log"
+fi
+echo "== bench"; date
+timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+cat "$OUT/bench.json"
+cd /tmp
+for NUM in ${NUMS:-fma exact}; do
+  echo "== rocprofv3 kernel trace $NUM"; date
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$NUM" -o run -- python3 "$ROOT/bench.py" --numerics $NUM --steps 20 --warmup 3 --cpu-sample 0 --alt-steps 0 > "$OUT/trace_$NUM.log" 2>&1 || { tail -30 "$OUT/trace_$NUM.log"; exit 1; }
+  tail -1 "$OUT/trace_$NUM.log"
+  find "$OUT/trace_$NUM" -name "*kernel_stats.csv" -exec cut -c1-200 {} \;
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== pmc $C $NUM"; date
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex window_kernel --output-format csv -d "$OUT/pmc_${C}_$NUM" -o run -- python3 "$ROOT/bench.py" --numerics $NUM --steps 5 --warmup 1 --cpu-sample 0 --alt-steps 0 > "$OUT/pmc_${C}_$NUM.log" 2>&1 || { tail -30 "$OUT/pmc_${C}_$NUM.log"; exit 1; }
+  done
+  python3 "$ROOT/tools/traffic_summary.py" --fetch "$OUT/pmc_FETCH_SIZE_$NUM" --write "$OUT/pmc_WRITE_SIZE_$NUM" \
+    --kernel window_kernel --workload-key "fused_dwt8_c3_int16_1000000_$NUM" \
+    --algorithmic-bytes 3476000000 --out "$OUT/traffic_$NUM.json"
+done
+echo "== done"; date
