@@ -32,6 +32,8 @@ BYTES_PER_EPOCH = 612 * 3 * 2 + 8 + 48 * 8   # whole path: 3,672 in + 8 marker +
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
+WINDOW_KERNEL = {"exact": "window_kernel<int16,3>", "fma": "window_kernel<int16,3>",
+                 "mfma": "mfma_window_kernel<int16,3>"}
 
 
 def parse():
@@ -40,7 +42,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
-    ap.add_argument("--numerics", choices=["exact", "fma"], default="fma",
+    ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
     ap.add_argument("--alt-steps", type=int, default=10,
@@ -144,7 +146,7 @@ def main():
     # the other numerics mode, same buffers (reported beside the headline, not as value)
     alt = None
     if args.alt_steps > 0:
-        other = "exact" if args.numerics == "fma" else "fma"
+        other = "exact" if args.numerics != "exact" else "fma"
         ctx.set_numerics(other)
         step()
         torch.cuda.synchronize(dev)
@@ -210,7 +212,7 @@ def main():
                 "epochs_per_gpu": n,
                 "channels": 3,
                 "numerics": args.numerics,
-                "kernels": ["baseline_kernel<int16,3>", "window_kernel<int16,3>"],
+                "kernels": ["baseline_kernel<int16,3>", WINDOW_KERNEL[args.numerics]],
                 "unit_rows_check": ok_norm,
             },
             "roofline": {
@@ -220,7 +222,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": (round(prof["hbm_bytes_per_launch"]) if prof else None),
-                "kernel": "window_kernel<int16,3>",
+                "kernel": WINDOW_KERNEL[args.numerics],
                 "kernel_ms": round(kernel_ms, 4),
                 "bytes_per_launch": kernel_bytes,
                 "bytes_per_epoch": kernel_bytes // n,

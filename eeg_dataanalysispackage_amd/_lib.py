@@ -30,6 +30,7 @@ MEM_HOST = 0
 MEM_DEVICE = 1
 EXACT = 0
 FMA = 1
+MFMA = 2
 PRESTIMULUS = 100
 POSTSTIMULUS = 750
 
@@ -91,6 +92,7 @@ SIGNATURES = {
     "eegfx_process_recording": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p,
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
+    "eegfx_dwt8_operator": (c_int, [c_void_p]),
     "eegfx_odp_create": (c_int, [c_void_p, POINTER(c_char_p), c_int32, POINTER(c_void_p)]),
     "eegfx_odp_load_data": (c_int, [c_void_p]),
     "eegfx_odp_error": (c_char_p, [c_void_p]),

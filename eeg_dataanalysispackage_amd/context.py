@@ -37,7 +37,9 @@ def _contig(a, dtype):
 
 class Context:
     """One HIP device + stream (eegfx_ctx).  numerics: "exact" (bit-exact to the reference
-    order of operations, default) or "fma" (fused multiply-add filter bank, <= 1e-9 relative)."""
+    order of operations, default), "fma" (fused multiply-add filter bank, <= 1e-9 relative) or
+    "mfma" (the window as one 16x512 fp64 operator on the matrix cores, <= 1e-9 relative; layouts
+    without a matrix kernel run the "fma" filter bank)."""
 
     def __init__(self, device: int = 0, numerics: str = "exact"):
         h = c_void_p()
@@ -54,7 +56,7 @@ class Context:
         return self._h
 
     def set_numerics(self, numerics: str) -> None:
-        mode = {"exact": _lib.EXACT, "fma": _lib.FMA}[numerics]
+        mode = {"exact": _lib.EXACT, "fma": _lib.FMA, "mfma": _lib.MFMA}[numerics]
         check(lib().eegfx_ctx_set_numerics(self.handle, mode))
         self.numerics = numerics
 
@@ -149,6 +151,15 @@ class Context:
         n_frames = dst.numel() // n_channels
         check(lib().eegfx_synth_recording(self.handle, ptr(dst), n_frames, n_channels,
                                           ctypes.c_uint64(seed)))
+
+
+def dwt8_operator() -> np.ndarray:
+    """The fe=dwt-8 window transform as a 16 x 512 matrix (host; eegfx_dwt8_operator):
+    row r of the first 16 coefficients (a6 ++ d6, before normalisation) of a window x is
+    ``M[r] @ x`` -- the operator the "mfma" numerics applies on the FP64 matrix cores."""
+    m = np.empty((16, 512), dtype=np.float64)
+    check(lib().eegfx_dwt8_operator(ptr(m)))
+    return m
 
 
 def device_count() -> int:

@@ -100,6 +100,21 @@ struct eegfx_ctx {
   std::vector<int64_t> event_bytes;
   size_t n_timed = 0;
   DevBuf raw, pos, out, scratch, fused;
+  DevBuf mop;  // dwt-8 operator rows for EEGFX_MFMA (uploaded on first use)
+  bool mop_ready = false;
+
+  const double* operator_rows() {
+    if (!mop_ready) {
+      std::vector<double> h(kOperatorRowDoubles);
+      dwt8_operator_rows(h.data());
+      void* d = mop.get(sizeof(double) * h.size());
+      HIP_CHECK(hipMemcpyAsync(d, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice,
+                               stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      mop_ready = true;
+    }
+    return (const double*)mop.p;
+  }
 
   void activate() const { HIP_CHECK(hipSetDevice(device)); }
   void tic() {
@@ -148,7 +163,18 @@ void check_mem(int mem) {
 void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_frames, int ct,
                            const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                            double* out) {
-  const bool fast = ctx->numerics == EEGFX_FMA;
+  const bool fast = ctx->numerics != EEGFX_EXACT;
+  if (ctx->numerics == EEGFX_MFMA && mfma_supported(fmt, ct, C) &&
+      n_frames * ct * 2 >= 16) {
+    const double* mrows = ctx->operator_rows();
+    void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
+    HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch));
+    ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
+    HIP_CHECK(launch_mfma_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch, mrows,
+                                 out));
+    ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
+    return;
+  }
   if (fused_supported(fmt, ct, C, out)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch));
@@ -423,7 +449,8 @@ int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream) {
 int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics) {
   return guarded([&] {
     if (!ctx) fail(EEGFX_EINVAL, "null context");
-    if (numerics != EEGFX_EXACT && numerics != EEGFX_FMA) fail(EEGFX_EINVAL, "numerics %d", numerics);
+    if (numerics != EEGFX_EXACT && numerics != EEGFX_FMA && numerics != EEGFX_MFMA)
+      fail(EEGFX_EINVAL, "numerics %d", numerics);
     ctx->numerics = numerics;
   });
 }
@@ -475,6 +502,7 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     ctx->out.release();
     ctx->scratch.release();
     ctx->fused.release();
+    ctx->mop.release();
     ctx->destroy_events();
     (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -549,7 +577,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
     double* d_out = mem == EEGFX_MEM_DEVICE ? out : (double*)ctx->out.get(out_bytes);
     ctx->tic();
     HIP_CHECK(launch_features_from_epochs(ctx->stream, d_in, n, C, skip, feature_size,
-                                          ctx->numerics == EEGFX_FMA, d_out));
+                                          ctx->numerics != EEGFX_EXACT, d_out));
     ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -581,6 +609,13 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
       HIP_CHECK(hipMemcpyAsync(features, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       HIP_CHECK(hipStreamSynchronize(ctx->stream));
     }
+  });
+}
+
+int eegfx_dwt8_operator(double* M) {
+  return guarded([&] {
+    if (!M) fail(EEGFX_EINVAL, "null argument");
+    dwt8_operator(M);
   });
 }
 
@@ -665,7 +700,7 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
     double* d_out = (double*)ctx->out.get(out_bytes);
     HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)odp->d_epochs.p,
                                           odp->n_epochs, 3, skip, feature_size,
-                                          ctx->numerics == EEGFX_FMA, d_out));
+                                          ctx->numerics != EEGFX_EXACT, d_out));
     HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
   });

@@ -38,6 +38,12 @@
 #include "dwt8.h"
 #include "launch.h"
 
+// Perf-study builds only (tools/probes/window_probe.hip): bit 0 drops the window DMA (and its
+// waits), bit 1 the LDS reads + decode, bit 2 the filter bank; the library is built with 0.
+#ifndef EEGFX_FUSED_ABLATION
+#define EEGFX_FUSED_ABLATION 0
+#endif
+
 namespace eegfx {
 namespace dev {
 
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   if (w == 0 && lane < kSub)
     tdelta[0][lane] = first + lane < n ? (int)(window_byte<CT>(pos, first + lane) & 15) : 0;
   float bcur = (first + el < n) ? base[(first + el) * C + w] : 0.0f;
-  if (dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane))
+  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane))
     dma_fixup<CT, C>(raw, nbytes, pos, n, first, win, w, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -324,12 +330,24 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       if (w == 0 && lane < kSub)
         tdelta[(kk + 1) & 1][lane] = e1 + lane < n ? (int)(window_byte<CT>(pos, e1 + lane) & 15) : 0;
       bcur = (e1 + el < n) ? base[(e1 + el) * C + w] : 0.0f;
-      need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane);
+      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane);
     }
     double x[kIn];
-    decode_pairs(xr, r, b, x);
+    if constexpr (EEGFX_FUSED_ABLATION & 2) {
+#pragma unroll
+      for (int k = 0; k < kIn; ++k) x[k] = (double)b + k;
+    } else {
+      decode_pairs(xr, r, b, x);
+    }
     double a6, d6;
-    dwt8_cascade<FAST, SHFL>(x, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
+    if constexpr (EEGFX_FUSED_ABLATION & 4) {
+      a6 = 0.0;
+#pragma unroll
+      for (int k = 0; k < kIn; ++k) a6 += x[k];
+      d6 = a6;
+    } else {
+      dwt8_cascade<FAST, SHFL>(x, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
+    }
     double* fb = feat[kk & 1];
     fb[el * F + w * 16 + s] = a6;
     fb[el * F + w * 16 + 8 + s] = d6;
@@ -342,6 +360,277 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   }
 }
 
+
+// ================================================================================================
+// engine_kernel -- the same sub-tile computation, decoupled from HBM by a loader wave.
+//
+// Persistent: one workgroup per CU = L loader waves + G groups of C consumer waves (wave c of a
+// group = channel c).  Every group owns one LDS window slot (8 epochs, ESTR_E dwords per epoch).
+// The workgroup's tiles i = 0, 1, 2, ... (tile = 8 epochs, global tile blockIdx.x + i*gridDim.x)
+// go to group i % G in round i / G and are fetched by loader i % L:
+//   loader:   wait until the group released its slot for the round (free[g] >= C*round) ->
+//             8 positions + 24 baselines by scalar loads -> misalignments + baselines into the
+//             slot header -> 32 unconditional LDS-DMA instructions (dummy lanes read the first
+//             quad of the recording into the slot's padding) -> wait for the PREVIOUS tile to
+//             land (s_waitcnt vmcnt(32): exactly one tile newer), patch its past-the-end quads,
+//             publish it (full[g] = round + 1).  Two tiles in flight per loader.
+//   consumer: wait full[g] > round -> copy its 72 samples to VGPRs -> release (free[g] += 1)
+//             -> decode + filter bank -> features into the group's LDS feature block ->
+//             progress word fdone[g][c] = round + 1; wave round % C waits for the group's
+//             words, normalises, stores.
+// Compute waves never issue or wait on HBM traffic, so loads overlap the filter bank across the
+// whole CU.  Flags live in LDS; every spin is bounded (a broken hand-off ends the kernel with
+// wrong rows -- caught by the parity tests -- instead of hanging the GPU).
+template <int CT>
+struct EngineGeo {
+  using G = Geometry<CT>;
+  static constexpr int PER_E = (G::EPQ + 63) / 64;         // 4 DMA instructions per epoch
+  static constexpr int NI = kSub * PER_E;                    // 32 per tile
+  static constexpr int ESTR_E = round_up_res(PER_E * 256, 32, 1);  // 1025 dwords: no DMA clobber
+  static constexpr int SLOT_DW = kSub * ESTR_E;
+};
+
+__device__ __forceinline__ uint32_t lds_addr32(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Publishes an LDS-DMA'd slot to the other waves: after the loader's covering vmcnt wait, one
+// read of the slot's last-written dword drains this CU's LDS write path before the flag store.
+__device__ __forceinline__ void publish_slot(uint32_t* flag, uint32_t v, const uint32_t* last) {
+  uint32_t t;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(lds_addr32(last)) : "memory");
+  (void)t;
+  lds_st(flag, v);
+}
+__device__ __forceinline__ void lds_inc(uint32_t* p) {
+  __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Bounded spin (~2^24 polls with s_sleep): false if the flag never reached v.
+__device__ __forceinline__ bool spin_ge(const uint32_t* p, uint32_t v) {
+  for (int k = 0; k < (1 << 24); ++k) {
+    if (lds_ld(p) >= v) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+template <int CT, int C>
+__device__ __forceinline__ void engine_fix(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                           const int64_t (&B)[kSub], int64_t e0, int64_t n,
+                                           uint32_t* win, int lane) {
+  using G = Geometry<CT>;
+  using E = EngineGeo<CT>;
+  for (int e = 0; e < kSub; ++e) {
+    if (e0 + e >= n) break;
+    for (int i = lane; i < G::EPQ; i += 64) {
+      const int sg = i / G::SEGQ, q = i - sg * G::SEGQ;
+      const int64_t A = (B[e] & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
+      if (A + 16 > nbytes) lds_store4(win + e * E::ESTR_E + 4 * i, load16(raw, nbytes, A));
+    }
+  }
+}
+
+// Meta ring: per batch of kMetaT consecutive tiles of the workgroup, the 8 positions (4 quads) and
+// 8*C baselines (2*C quads) of each tile, fetched by one LDS-DMA instruction (lane = quad).
+// Ring depth: batch b + kMetaR reuses batch b's slot; it is fetched at tile kMetaT*(b + kMetaR - 2),
+// by which time the loader has seen every tile of batch b released (each group releases a tile
+// right after reading its meta, and the loader is at most G tiles ahead of the releases):
+// kMetaT*(kMetaR - 2) >= G + kMetaT - 1.
+constexpr int kMetaT = 4;
+constexpr int kMetaR = 4;
+constexpr int kMetaQ = 64;  // quads per batch slot (one DMA instruction)
+__device__ __forceinline__ const int64_t* meta_pos(const uint32_t* mring, int64_t i) {
+  return (const int64_t*)(mring + ((i / kMetaT) % kMetaR) * kMetaQ * 4 + (i % kMetaT) * 16);
+}
+__device__ __forceinline__ const float* meta_base(const uint32_t* mring, int64_t i) {
+  return (const float*)(mring + ((i / kMetaT) % kMetaR) * kMetaQ * 4 + kMetaT * 16) +
+         (i % kMetaT) * kSub * 3;
+}
+// Lanes 0..4*kMetaT-1: positions (quad q of tile t = lane/4); lanes 16..16+2*C*kMetaT-1:
+// baselines.  Out-of-range quads read the first quad of the recording (discarded).
+template <int C>
+__device__ __forceinline__ void dma_meta_batch(const uint8_t* __restrict__ raw,
+                                               const int64_t* __restrict__ pos,
+                                               const float* __restrict__ base, int64_t n,
+                                               int64_t ntl, int64_t batch, uint32_t* dst, int lane) {
+  static_assert(C == 3, "meta layout assumes 3 channels");
+  const uint8_t* src = raw;
+  if (lane < 4 * kMetaT) {
+    const int64_t i = batch * kMetaT + lane / 4;
+    const int64_t e = ((int64_t)blockIdx.x + i * gridDim.x) * kSub + 2 * (lane % 4);
+    if (i < ntl && e + 1 < n) src = (const uint8_t*)(pos + e);
+  } else if (lane < 4 * kMetaT + 2 * C * kMetaT) {
+    const int k = lane - 4 * kMetaT;
+    const int64_t i = batch * kMetaT + k / (2 * C);
+    const int64_t f = ((int64_t)blockIdx.x + i * gridDim.x) * kSub * C + 4 * (k % (2 * C));
+    if (i < ntl && f + 3 < n * C) src = (const uint8_t*)(base + f);
+  }
+  dma16(src, dst);
+}
+
+// Some window quad of the tile reaches past the recording (its DMA lane read a dummy quad).
+template <int CT>
+__device__ __forceinline__ bool tile_late(const int64_t (&B)[kSub], int64_t nbytes) {
+  bool late = false;
+#pragma unroll
+  for (int e = 0; e < kSub; ++e) late |= (B[e] & ~(int64_t)15) + 16 * 8 * Geometry<CT>::SEGQ > nbytes;
+  return late;
+}
+
+template <int CT, int C, bool FAST, int G_, int L>
+__global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
+    const float* __restrict__ base, int64_t n, double* __restrict__ out) {
+  using G = Geometry<CT>;
+  using E = EngineGeo<CT>;
+  constexpr int F = C * 16;
+  __shared__ __attribute__((aligned(16))) uint32_t win[G_][E::SLOT_DW];
+  __shared__ __attribute__((aligned(16))) double feat[G_][2][kSub * F];
+  __shared__ double norm[G_][kSub];
+  __shared__ __attribute__((aligned(16))) uint32_t mring[kMetaR * kMetaQ * 4];
+  static_assert(kMetaT * (kMetaR - 2) >= G_ + kMetaT - 1, "meta ring too shallow");
+  __shared__ uint32_t full[G_], freed[G_], fdone[G_][C];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < G_) {
+    full[tid] = 0;
+    freed[tid] = 0;
+  }
+  if (tid < G_ * C) fdone[tid / C][tid % C] = 0;
+  __syncthreads();  // the only workgroup barrier
+  const int64_t nbytes = n_frames * G::FB;
+  const int64_t ntiles = (n + kSub - 1) / kSub;
+  const int64_t ntl = ntiles > blockIdx.x ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  auto tile_e0 = [&](int64_t i) { return ((int64_t)blockIdx.x + i * gridDim.x) * kSub; };
+
+  if (w >= G_ * C) {  // ---------------------------------------------------------------- loader
+    // Every vector-memory op of this wave is an LDS-DMA with a known count, so `s_waitcnt
+    // vmcnt(N)` waits for exactly one earlier tile; nothing in the loop waits on SMEM.
+    bool pending = false, ok = true;
+    int pg = 0, pround = 0;
+    int64_t pe0 = 0;
+    int64_t pB[kSub];
+    int32_t qoff[E::PER_E];  // byte offset of this lane's quad in DMA instruction j of an epoch
+#pragma unroll
+    for (int j = 0; j < E::PER_E; ++j) {
+      const int i2 = 64 * j + lane, sg = i2 / G::SEGQ, q = i2 - sg * G::SEGQ;
+      qoff[j] = i2 < G::EPQ ? kSegLen * G::FB * sg + 16 * q : 0;
+    }
+    for (int b0 = 0; b0 < 2; ++b0)  // meta of the first two batches
+      dma_meta_batch<C>(raw, pos, base, n, ntl, b0, mring + b0 * kMetaQ * 4, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int64_t i = 0; i < ntl && ok; ++i) {
+      const int g = (int)(i % G_);
+      const int round = (int)(i / G_);
+      const int64_t e0 = tile_e0(i);
+      const bool batch_start = (i % kMetaT) == 0;
+      ok = spin_ge(&freed[g], (uint32_t)(C * round));
+      if (e0 + kSub > n) {  // the last tile: quads straddling the end of pos[]/base[] were dummies
+        int64_t* wp = (int64_t*)meta_pos(mring, i);
+        float* wb = (float*)meta_base(mring, i);
+        if (lane < kSub && e0 + lane < n) wp[lane] = pos[e0 + lane];
+        if (lane < kSub * C && e0 * C + lane < n * C) wb[lane] = base[e0 * C + lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_sync();
+      }
+      const int64_t* mp = meta_pos(mring, i);
+      int64_t B[kSub];
+#pragma unroll
+      for (int e = 0; e < kSub; ++e) B[e] = e0 + e < n ? (mp[e] + 175) * G::FB : 0;
+      if (batch_start)  // meta of batch i/kMetaT + 2
+        dma_meta_batch<C>(raw, pos, base, n, ntl, i / kMetaT + 2,
+                          mring + ((i / kMetaT + 2) % kMetaR) * kMetaQ * 4, lane);
+      uint32_t* wn = win[g];
+      if (e0 + kSub <= n && !tile_late<CT>(B, nbytes)) {
+        // fast path: per-lane quad offsets are loop invariants; padding lanes re-read the
+        // epoch's first quad (no select, no bounds test)
+#pragma unroll
+        for (int m = 0; m < E::NI; ++m) {
+          const int e = m / E::PER_E, j = m - e * E::PER_E;
+          const uint8_t* eb = raw + (B[e] & ~(int64_t)15);
+          if constexpr (!(EEGFX_FUSED_ABLATION & 8)) dma16(eb + qoff[j], wn + e * E::ESTR_E + 256 * j);
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < E::NI; ++m) {
+          const int e = m / E::PER_E, j = m - e * E::PER_E;
+          const int i2 = 64 * j + lane;
+          const int sg = i2 / G::SEGQ, q = i2 - sg * G::SEGQ;
+          const int64_t A = (B[e] & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
+          const bool okq = e0 + e < n && i2 < G::EPQ && A + 16 <= nbytes;
+          if constexpr (!(EEGFX_FUSED_ABLATION & 8)) dma16(raw + (okq ? A : 0), wn + e * E::ESTR_E + 256 * j);
+        }
+      }
+      if (pending) {  // the previous tile: exactly its successor's DMAs (+ one meta DMA) are newer
+        if (batch_start) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E::NI + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E::NI) : "memory");
+        if (tile_late<CT>(pB, nbytes)) engine_fix<CT, C>(raw, nbytes, pB, pe0, n, win[pg], lane);
+        publish_slot(&full[pg], (uint32_t)(pround + 1), win[pg] + E::SLOT_DW - 1);
+      }
+      pending = true;
+      pg = g;
+      pround = round;
+      pe0 = e0;
+#pragma unroll
+      for (int e = 0; e < kSub; ++e) pB[e] = B[e];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pending) {
+      if (tile_late<CT>(pB, nbytes)) engine_fix<CT, C>(raw, nbytes, pB, pe0, n, win[pg], lane);
+      publish_slot(&full[pg], (uint32_t)(pround + 1), win[pg] + E::SLOT_DW - 1);
+    }
+    return;
+  }
+
+  // ----------------------------------------------------------------------------------- consumer
+  const int g = w / C, c = w - g * C;
+  const int el = lane >> 3, s = lane & 7;
+  const int col = sel.col[c];
+  const float r = sel.res[c];
+  for (int64_t i = g, round = 0; i < ntl; i += G_, ++round) {
+    const int64_t e0 = (blockIdx.x + i * gridDim.x) * kSub;
+    if (!spin_ge(&full[g], (uint32_t)(round + 1))) return;
+    const int64_t* mp = meta_pos(mring, i);
+    const int dl = e0 + el < n ? (int)(((mp[el] + 175) * G::FB) & 15) : 0;
+    const uint8_t* eb = (const uint8_t*)(win[g] + el * E::ESTR_E) + dl + 2 * col;
+    const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
+    const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
+    int16_t xr[kIn];
+#pragma unroll
+    for (int k = 0; k < kSegLen; ++k) xr[k] = own[k * CT];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nxt[k * CT];
+    const float b = meta_base(mring, i)[el * C + c];
+    lds_inc(&freed[g]);  // DS ops of a wave complete in order: the reads above are done
+    double a6, d6;
+    if constexpr (EEGFX_FUSED_ABLATION & 16) {
+      a6 = (double)xr[0] + b;
+      d6 = (double)xr[kIn - 1];
+    } else {
+      double x[kIn];
+      decode_pairs(xr, r, b, x);
+      dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
+    }
+    double* fb = feat[g][round & 1];
+    fb[el * F + c * 16 + s] = a6;
+    fb[el * F + c * 16 + 8 + s] = d6;
+    lds_st(&fdone[g][c], (uint32_t)(round + 1));
+    if (!(EEGFX_FUSED_ABLATION & 32) && c == (int)(round % C)) {
+      // per-wave progress words: a wave may already be one round ahead, so a shared counter
+      // could be satisfied before this round's features are all written
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < C; ++k) ok = ok && spin_ge(&fdone[g][k], (uint32_t)(round + 1));
+      if (!ok) return;
+      normalise_store<F>(fb, norm[g], out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
+    }
+  }
+}
 }  // namespace dev
 
 namespace {
@@ -389,6 +678,32 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
 }
 }  // namespace
 
+template <bool FAST, int G_, int L>
+hipError_t launch_engine3(hipStream_t st, const void* raw, int64_t n_frames, const ChanSel& sel,
+                          const int64_t* pos, const float* base, int64_t n, double* out) {
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const int64_t ntiles = (n + dev::kSub - 1) / dev::kSub;
+  const int64_t grid = ntiles < cus ? ntiles : cus;
+  hipLaunchKernelGGL((dev::engine_kernel<3, 3, FAST, G_, L>), dim3((unsigned)grid),
+                     dim3(64 * (L + G_ * 3)), 0, st, (const uint8_t*)raw, n_frames, sel, pos, base,
+                     n, out);
+  return hipGetLastError();
+}
+
+// The loader/consumer engine is opt-in (EEGFX_ENGINE=1): parity-green, but slower than
+// window_kernel on MI355X so far (DESIGN.md "Alternatives measured").
+bool engine_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("EEGFX_ENGINE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 bool fused_supported(int fmt, int ct, int C, const double* out) {
   return fmt == 0 && ct == 3 && C == 3 && ((uintptr_t)out & 15) == 0;
 }
@@ -415,6 +730,17 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
                                const void* scratch, double* out) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
+  if (engine_enabled() && n_frames * ct * 2 >= 16) {
+    const char* gv = getenv("EEGFX_ENGINE_G");
+    const int gsel = gv ? atoi(gv) : 3;
+    if (fast)
+      return gsel == 4 ? launch_engine3<true, 4, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
+           : gsel == 2 ? launch_engine3<true, 3, 2>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
+                       : launch_engine3<true, 3, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
+    return gsel == 4 ? launch_engine3<false, 4, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
+         : gsel == 2 ? launch_engine3<false, 3, 2>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
+                     : launch_engine3<false, 3, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
+  }
   if (fast) launch_window3<true>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
   else launch_window3<false>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
   return hipGetLastError();

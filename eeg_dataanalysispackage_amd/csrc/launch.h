@@ -38,4 +38,16 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);
 
+// Collapsed-operator window on the FP64 matrix cores (mfma.hip), the EEGFX_MFMA numerics: same
+// baseline scratch as the fused path; mrows = dwt8_operator_rows() on the device (8 KB).
+bool mfma_supported(int fmt, int ct, int C);
+hipError_t launch_mfma_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
+                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                              const void* scratch, const double* mrows, double* out);
+// dwt8_operator.cpp: M[16][512] with coefficient r = sum_k M[r][k] x[k] (a6 ++ d6); M is
+// block-circulant, rows[0][.] = M[0][.] (a6[0]) and rows[1][.] = M[8][.] (d6[0]) define it.
+void dwt8_operator(double* M);
+void dwt8_operator_rows(double* rows);
+constexpr int kOperatorRowDoubles = 2 * 512;
+
 }  // namespace eegfx

@@ -63,6 +63,8 @@ extern "C" {
 /* numerics of the DWT filter bank */
 #define EEGFX_EXACT 0   /* separate fp64 mul + add in the reference order: bit-exact to Java */
 #define EEGFX_FMA 1     /* fp64 fused multiply-add: within 1e-9 relative, fewer instructions  */
+#define EEGFX_MFMA 2    /* window as one 16x512 fp64 operator on the matrix cores: within 1e-9;
+                         * falls back to EEGFX_FMA where no matrix kernel covers the layout    */
 
 typedef struct eegfx_ctx eegfx_ctx;
 typedef struct eegfx_odp eegfx_odp;
@@ -76,7 +78,7 @@ int eegfx_ctx_create(int device, eegfx_ctx** out);
 /* Makes the context enqueue on `hip_stream` (hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. */
 int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream);
-int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | EEGFX_FMA */
+int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | _FMA | _MFMA */
 int eegfx_ctx_synchronize(eegfx_ctx* ctx);
 /* Kernel timing for the roofline leg of bench.py.  While enabled, every compute call brackets its
  * dominant kernel (window_kernel for the fused path) with a pair of HIP events on the context
@@ -168,6 +170,12 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
                             int32_t n_channels_total, const int32_t* cols, const float* res,
                             int32_t C, const int64_t* pos, int64_t n_epochs, double* features,
                             int mem);
+
+/* The fe=dwt-8 window transform as a matrix (host only, no device): M[16][512] row-major with
+ * coefficient r of WaveletTransform's first 16 (a6[0..7] ++ d6[0..7], before normalisation)
+ * = sum_k M[r][k] * epoch[c][175 + k].  This is the operator EEGFX_MFMA applies on the FP64
+ * matrix cores (long-double evaluation of the reference pyramid, rounded once). */
+int eegfx_dwt8_operator(double* M);
 
 /* Deterministic synthetic multiplexed int16 recording, generated on device:
  * DC -25000 counts + bounded random walk + 10 Hz sinusoid, clipped to int16.  dst is a device

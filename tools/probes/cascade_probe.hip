@@ -41,5 +41,9 @@ int main() {
   printf("exact lds  minw3: %.3f ms\n", run<false, false, 3>(out, npairs));
   printf("fma   lds  minw3: %.3f ms\n", run<true, false, 3>(out, npairs));
   printf("exact shfl minw2: %.3f ms\n", run<false, true, 2>(out, npairs));
+  printf("fma   shfl minw2: %.3f ms\n", run<true, true, 2>(out, npairs));
+  printf("fma   shfl minw3: %.3f ms\n", run<true, true, 3>(out, npairs));
+  printf("fma   lds  minw2: %.3f ms\n", run<true, false, 2>(out, npairs));
+  printf("fma   shfl minw1: %.3f ms\n", run<true, true, 1>(out, npairs));
   return 0;
 }

@@ -1,0 +1,41 @@
+// Probe: window_kernel (VALU cascade, fma numerics) timing under EEGFX_FUSED_ABLATION (bit 0: no
+// window DMA, bit 1: no LDS reads/decode, bit 2: no filter bank) on the bench workload.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../../eeg_dataanalysispackage_amd/csrc/fused.hip"
+
+int main() {
+  const int64_t n = 1000000, nf = 1000 * n + 2000;
+  uint8_t* raw;
+  int64_t* pos;
+  float* base;
+  double* out;
+  (void)hipMalloc(&raw, nf * 6);
+  (void)hipMalloc(&pos, n * 8);
+  (void)hipMalloc(&base, n * 12);
+  (void)hipMalloc(&out, n * 48 * 8);
+  (void)hipMemset(raw, 3, nf * 6);
+  std::vector<int64_t> hp(n);
+  for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + 1000 * i;
+  (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
+  eegfx::ChanSel sel{};
+  for (int c = 0; c < 3; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
+  (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int r = 0; r < 2; ++r)
+    (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, true, base, out);
+  (void)hipEventRecord(a);
+  for (int r = 0; r < 10; ++r)
+    (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, true, base, out);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms;
+  (void)hipEventElapsedTime(&ms, a, b);
+  printf("window ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, ms / 10);
+  return 0;
+}
