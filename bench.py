@@ -28,12 +28,24 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "epochs/sec feature-extracted (whole node) + % HBM roofline, 1/2/4/8 GPUs"
-BYTES_PER_EPOCH = 612 * 3 * 2 + 8 + 48 * 8   # whole path: 3,672 in + 8 marker + 384 out (8d)
+
+
+def bytes_per_epoch(ct, C):
+    """Whole-path algorithmic bytes: 612 frames in + 8 B marker + 16*C doubles out
+    (3 ch: 4,064 B; 32 ch: 43,272 B)."""
+    return 612 * ct * 2 + 8 + 16 * C * 8
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
 WINDOW_KERNEL = {"exact": "window_kernel<int16,3>", "fma": "window_kernel<int16,3>",
                  "mfma": "mfma_window_kernel<int16,3>"}
+WORKLOADS = {
+    "c3": {"ct": 3, "C": 3, "desc": "configs[1]: synthetic 1M epochs x 3 ch (Fz/Cz/Pz) multiplexed "
+                                    "int16 @1000 Hz -> fe=dwt-8 48-dim L2-normalised features, per GPU"},
+    "c32": {"ct": 32, "C": 32, "desc": "configs[3]: synthetic epochs x full 32-channel montage, "
+                                       "multiplexed int16 @1000 Hz, every channel through the DWT -> "
+                                       "512-dim L2-normalised features, per GPU"},
+}
 
 
 def parse():
@@ -42,6 +54,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
+    ap.add_argument("--workload", choices=["c3", "c32"], default="c3",
+                    help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "
+                         "32-channel montage, every channel through the DWT, 512-dim)")
     ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
@@ -91,6 +106,10 @@ def main():
 
     import eeg_dataanalysispackage_amd as fx
 
+    wl = WORKLOADS[args.workload]
+    ct, C = wl["ct"], wl["C"]
+    if args.workload == "c32" and args.epochs == 1_000_000:
+        args.epochs = 250_000  # 16 GB recording + 1 GB of 512-dim features per GPU
     n = args.epochs
     n_frames = FRAMES_PER_EPOCH * n + 2000
     ctx = fx.Context(local, numerics=args.numerics)
@@ -100,15 +119,15 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
-    raw = torch.empty((n_frames, 3), dtype=torch.int16, device=dev)
-    ctx.synth_recording(raw, 3, SEED + rank)
+    raw = torch.empty((n_frames, ct), dtype=torch.int16, device=dev)
+    ctx.synth_recording(raw, ct, SEED + rank)
     pos = torch.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (n + 1), FRAMES_PER_EPOCH,
                        dtype=torch.int64, device=dev)
-    out = torch.empty((n, 48), dtype=torch.float64, device=dev)
-    cols, res = [0, 1, 2], [0.1, 0.1, 0.1]
+    out = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
+    cols, res = list(range(C)), [0.1] * C
 
     def step():
-        ctx.process_recording(raw, 3, cols, res, pos, out=out)
+        ctx.process_recording(raw, ct, cols, res, pos, out=out)
 
     for _ in range(args.warmup):
         step()
@@ -179,19 +198,22 @@ def main():
         torch.cuda.synchronize(dev)
         gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        gather = {"op": "all_gather_into_tensor", "bytes_per_rank": n * 48 * 8,
+        gather = {"op": "all_gather_into_tensor", "bytes_per_rank": n * 16 * C * 8,
                   "ms": round(float(gt[0]) * 1e3, 3)}
         del full
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args, raw, out)
+        cpu = cpu_baseline(args, raw, out, ct, C)
 
     if rank == 0:
-        workload_key = f"fused_dwt8_c3_int16_{n}_{args.numerics}"
+        workload_key = f"fused_dwt8_c{C}_int16_{n}_{args.numerics}"
         value = world * n * args.steps / elapsed
         achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9
-        path_gbs = n * BYTES_PER_EPOCH / (step_ms * 1e-3) / 1e9
+        bpe = bytes_per_epoch(ct, C)
+        path_gbs = n * bpe / (step_ms * 1e-3) / 1e9
+        kernels = (["baseline_kernel<int16,3>", WINDOW_KERNEL[args.numerics]] if C == 3 else
+                   ["baseline_any_kernel<int16>", "window_wide_kernel<int16>"])
         prof = traffic_from_profiles(workload_key)
         line = {
             "metric": METRIC,
@@ -207,12 +229,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": "configs[1]: synthetic 1M epochs x 3 ch (Fz/Cz/Pz) multiplexed int16 "
-                            "@1000 Hz -> fe=dwt-8 48-dim L2-normalised features, per GPU",
+                "workload": wl["desc"],
                 "epochs_per_gpu": n,
-                "channels": 3,
+                "channels": C,
                 "numerics": args.numerics,
-                "kernels": ["baseline_kernel<int16,3>", WINDOW_KERNEL[args.numerics]],
+                "kernels": kernels,
                 "unit_rows_check": ok_norm,
             },
             "roofline": {
@@ -222,12 +243,12 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": (round(prof["hbm_bytes_per_launch"]) if prof else None),
-                "kernel": WINDOW_KERNEL[args.numerics],
+                "kernel": kernels[1],
                 "kernel_ms": round(kernel_ms, 4),
                 "bytes_per_launch": kernel_bytes,
                 "bytes_per_epoch": kernel_bytes // n,
                 "traffic_source": (prof.get("source") if prof else None),
-                "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": BYTES_PER_EPOCH,
+                "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": bpe,
                                "GBps": round(path_gbs, 1),
                                "frac": round(path_gbs / HBM_PEAK_GBS, 4)},
             },
@@ -244,18 +265,19 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, raw, gpu_out):
+def cpu_baseline(args, raw, gpu_out, ct, C):
     """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
     threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload."""
     from oracle import oracle
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    k = min(args.cpu_sample, args.epochs)
+    k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10, args.epochs)
     host = raw[: FRAMES_PER_EPOCH * k + 2000].cpu().numpy()
     pos = np.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (k + 1), FRAMES_PER_EPOCH, dtype=np.int64)
-    oracle.process_recording(host[: FRAMES_PER_EPOCH * 200 + 2000], [0, 1, 2], [0.1] * 3,
+    cols = list(range(C))
+    oracle.process_recording(host[: FRAMES_PER_EPOCH * 200 + 2000], cols, [0.1] * C,
                              pos[:200], faithful=True, nthreads=threads)  # warm-up
     t0 = time.perf_counter()
-    feats = oracle.process_recording(host, [0, 1, 2], [0.1] * 3, pos, faithful=True,
+    feats = oracle.process_recording(host, cols, [0.1] * C, pos, faithful=True,
                                      nthreads=threads)
     dt = time.perf_counter() - t0
     gpu = gpu_out[:k].cpu().numpy()

@@ -184,6 +184,16 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
     ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
     return;
   }
+  if (wide_supported(fmt, ct, C)) {
+    void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
+    HIP_CHECK(launch_baseline_any(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fscratch));
+    ctx->tic();
+    HIP_CHECK(launch_window_wide(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast,
+                                 fscratch, out));
+    const int64_t elem = fmt == EEGFX_INT_16 ? 2 : 4;
+    ctx->toc(n * (EEGFX_DWT8_EPOCH_SIZE * ct * elem + C * 4 + 8 + C * 16 * 8));
+    return;
+  }
   double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
   ctx->tic();
   HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep));

@@ -670,6 +670,7 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
     launched = true;                                                                              \
   }
   EEGFX_D(4, 1, true) EEGFX_D(3, 1, true) EEGFX_D(2, 2, true) EEGFX_D(3, 2, true)
+  EEGFX_D(4, 2, true) EEGFX_D(4, 4, true) EEGFX_D(4, 8, true) EEGFX_D(3, 4, true)
   EEGFX_D(3, 1, false) EEGFX_D(3, 2, false)
 #undef EEGFX_D
   if (!launched)

@@ -38,6 +38,17 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);
 
+// Any-layout fused path (wide.hip): baseline_any_kernel then window_wide_kernel, same scratch
+// contract as the 3-channel kernels.  wide_supported: int16/float32, C <= 64, one epoch's staged
+// window + features within 64 KB of LDS (int16: about 60 channels in the file).
+bool wide_supported(int fmt, int ct, int C);
+hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                               void* scratch);
+hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                              const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
+                              const void* scratch, double* out);
+
 // Collapsed-operator window on the FP64 matrix cores (mfma.hip), the EEGFX_MFMA numerics: same
 // baseline scratch as the fused path; mrows = dwt8_operator_rows() on the device (8 KB).
 bool mfma_supported(int fmt, int ct, int C);

@@ -1,0 +1,217 @@
+// wide.hip -- fused raw -> features for any multiplexed layout (any channel count, any selected
+// channels, int16 or float32 samples): BASELINE.json configs[3], the 32-channel montage with all
+// channels through the DWT (512-dim features), and every layout the 3-channel kernels of fused.hip
+// do not cover.
+//
+//   baseline_any_kernel   a5 + a6 prefix: lane = (epoch, selected channel) folds its 100
+//                         pre-stimulus samples sequentially in fp32 (Baseline.java:29-42); for a
+//                         multiplexed file the lanes of one epoch read adjacent samples of a frame.
+//   window_wide_kernel    a3 + a7 + a11..a13 for EPW epochs per workgroup: the 512-frame windows
+//                         are staged in LDS as 8 segment blocks of 64 frames (block s = global
+//                         quads floor16(B) + 64*FB*s + 16*i, i <= 4*FB: the +1 quad absorbs the
+//                         window's misalignment, and the block stride is 4 (mod 32) dwords so the
+//                         8 segments of a half-wave sit on distinct banks), then the dwt8.h
+//                         filter bank runs with wave lanes = 8 signals x 8 segments, signals =
+//                         (epoch, channel) pairs, and the rows are normalised with the
+//                         reference's sequential sum of squares (EXACT) or a lane-parallel one
+//                         (FMA) before one coalesced store.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dwt8.h"
+#include "launch.h"
+
+namespace eegfx {
+namespace dev {
+
+typedef uint32_t wq_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t wq_a16 __attribute__((ext_vector_type(4), aligned(16)));
+
+template <typename T>
+__global__ __launch_bounds__(256) void baseline_any_kernel(const T* __restrict__ raw, int64_t n_frames,
+                                                           int ct, ChanSel sel, int C,
+                                                           const int64_t* __restrict__ pos,
+                                                           int64_t n, float* __restrict__ bout) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * C) return;
+  const int64_t e = idx / C;
+  const int c = (int)(idx - e * C);
+  const int64_t lo = pos[e] - kPre;
+  const int col = sel.col[c];
+  const float r = sel.res[c];
+  float b = 0.0f;
+  for (int i = 0; i < kPre; ++i) {
+    const int64_t f = lo + i;
+    const float v = (f >= 0 && f < n_frames) ? (float)raw[f * ct + col] * r : 0.0f;
+    b = b + v;
+  }
+  bout[idx] = b / (float)kPre;
+}
+
+// One 16-byte quad of the recording at byte offset A (16-aligned), zero past the end.
+__device__ __forceinline__ wq_a4 wide_load16(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                             int64_t A) {
+  if (A + 16 <= nbytes) return *(const wq_a16*)(raw + A);
+  wq_a4 v = {0u, 0u, 0u, 0u};
+  if (A < nbytes) {
+    uint32_t t[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; i < 4; ++i) {
+      const int64_t a = A + 4 * i;
+      if (a + 4 <= nbytes) t[i] = *(const uint32_t*)(raw + a);
+      else if (a + 2 <= nbytes) t[i] = *(const uint16_t*)(raw + a);
+    }
+    v.x = t[0]; v.y = t[1]; v.z = t[2]; v.w = t[3];
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ float sample_at(const uint8_t* p) {
+  return (float)*(const T*)p;
+}
+
+// Per-workgroup LDS: EPW epochs x 8 segment blocks of SEGQ quads, then EPW x F features, then
+// EPW norms.  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame.
+template <typename T, bool FAST, int EPW>
+__global__ __launch_bounds__(256) void window_wide_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
+    double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int FB = ct * (int)sizeof(T);
+  const int SEGQ = 4 * FB + 1;
+  const int EQ = 8 * SEGQ;
+  const int F = 16 * C;
+  uint8_t* win = smem;
+  double* feat = (double*)(smem + (size_t)EPW * EQ * 16);
+  double* norm = feat + EPW * F;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t e0 = (int64_t)blockIdx.x * EPW;
+  const int ne = (n - e0) < EPW ? (int)(n - e0) : EPW;
+  const int64_t nbytes = n_frames * FB;
+
+  // stage the windows: quad i of epoch m = global quad floor16(B_m) + 64*FB*(i/SEGQ) + 16*(i%SEGQ)
+  for (int i = tid; i < ne * EQ; i += blockDim.x) {
+    const int m = i / EQ, iq = i - m * EQ;
+    const int sg = iq / SEGQ, q = iq - sg * SEGQ;
+    const int64_t B = (pos[e0 + m] + 175) * FB;
+    const int64_t A = (B & ~(int64_t)15) + (int64_t)64 * FB * sg + 16 * q;
+    const wq_a4 v = wide_load16(raw, nbytes, A);
+    uint32_t* d = (uint32_t*)(win + (size_t)i * 16);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+
+  // filter bank: signal = (epoch m, channel c), 8 per wave per pass
+  const int sig_lane = lane >> 3, s = lane & 7;
+  const int nsig = ne * C;
+  for (int sig0 = w * 8; sig0 < nsig; sig0 += 32) {  // uniform per wave
+    const int sig = sig0 + sig_lane;
+    const bool valid = sig < nsig;
+    const int m = valid ? sig / C : 0, c = valid ? sig - m * C : 0;
+    const int64_t B = (pos[e0 + m] + 175) * FB;
+    const uint8_t* eb = win + (size_t)m * EQ * 16 + (int)(B & 15) + sel.col[c] * (int)sizeof(T);
+    const uint8_t* own = eb + 16 * SEGQ * s;
+    const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
+    const float r = sel.res[c];
+    const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
+    double x[kIn];
+#pragma unroll
+    for (int k = 0; k < kSegLen; ++k) x[k] = (double)(sample_at<T>(own + k * FB) * r - b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[kSegLen + k] = (double)(sample_at<T>(nxt + k * FB) * r - b);
+    double a6, d6;
+    dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
+    if (valid) {
+      feat[m * F + c * 16 + s] = a6;
+      feat[m * F + c * 16 + 8 + s] = d6;
+    }
+  }
+  __syncthreads();
+
+  // SignalProcessing.normalize (SignalProcessing.java:38-52)
+  if constexpr (FAST) {
+    // lane-parallel sum of squares per epoch (order-free: the FMA contract is 1e-9)
+    for (int m = w; m < ne; m += blockDim.x / 64) {
+      double acc = 0.0;
+      for (int i = lane; i < F; i += 64) acc = __builtin_fma(feat[m * F + i], feat[m * F + i], acc);
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) norm[m] = sqrt(acc);
+    }
+  } else {
+    // the reference's sequential fold, index order, one lane per epoch
+    if (tid < ne) {
+      double acc = 0.0;
+      for (int i = 0; i < F; ++i) {
+        const double f = feat[tid * F + i];
+        acc = acc + f * f;
+      }
+      norm[tid] = sqrt(acc);
+    }
+  }
+  __syncthreads();
+  double* o = out + e0 * F;
+  for (int i = tid; i < ne * F; i += blockDim.x) o[i] = feat[i] / norm[i / F];
+}
+
+}  // namespace dev
+
+namespace {
+template <typename T, bool FAST, int EPW>
+hipError_t launch_wide_t(hipStream_t st, const void* raw, int64_t n_frames, int ct,
+                         const ChanSel& sel, int C, const int64_t* pos, const float* base,
+                         int64_t n, double* out) {
+  const int FB = ct * (int)sizeof(T);
+  const size_t lds = (size_t)EPW * 8 * (4 * FB + 1) * 16 + (size_t)EPW * 16 * C * 8 + EPW * 8;
+  const dim3 grid((unsigned)((n + EPW - 1) / EPW));
+  hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW>), grid, dim3(256), lds, st,
+                     (const uint8_t*)raw, n_frames, ct, sel, C, pos, base, n, out);
+  return hipGetLastError();
+}
+}  // namespace
+
+// LDS of one epoch's staged window + features; the wide kernel runs two epochs per workgroup
+// while that fits comfortably (two or more workgroups per CU), one otherwise.
+static size_t wide_lds_per_epoch(int fmt, int ct, int C) {
+  const int FB = ct * (fmt == 0 ? 2 : 4);
+  return (size_t)8 * (4 * FB + 1) * 16 + (size_t)16 * C * 8 + 8;
+}
+
+bool wide_supported(int fmt, int ct, int C) {
+  return (fmt == 0 || fmt == 1) && C >= 1 && C <= kMaxChannels && ct >= 1 &&
+         wide_lds_per_epoch(fmt, ct, C) <= 64 * 1024;
+}
+
+hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                               void* scratch) {
+  if (n == 0) return hipSuccess;
+  const dim3 grid((unsigned)((n * C + 255) / 256));
+  if (fmt == 0)
+    hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), 0, st,
+                       (const int16_t*)raw, n_frames, ct, sel, C, pos, n, (float*)scratch);
+  else
+    hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), 0, st, (const float*)raw,
+                       n_frames, ct, sel, C, pos, n, (float*)scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                              const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
+                              const void* scratch, double* out) {
+  if (n == 0) return hipSuccess;
+  const float* base = (const float*)scratch;
+  const bool two = wide_lds_per_epoch(fmt, ct, C) <= 32 * 1024;  // dynamic LDS stays <= 64 KB
+#define EEGFX_W(T, FA)                                                                        \
+  return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out)       \
+             : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
+  if (fmt == 0) {
+    if (fast) { EEGFX_W(int16_t, true) } else { EEGFX_W(int16_t, false) }
+  } else {
+    if (fast) { EEGFX_W(float, true) } else { EEGFX_W(float, false) }
+  }
+#undef EEGFX_W
+}
+
+}  // namespace eegfx

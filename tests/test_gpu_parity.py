@@ -231,3 +231,17 @@ def test_errors_are_raised(ctx):
         ctx.extract_features(np.zeros((2, 3, 750)), epoch_size=256)
     assert e.value.code == -7
     assert ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, []).shape == (0, 48)
+
+
+# ---- any-layout fused kernels (wide.hip): configs[3] 32-channel montage, fma numerics ---------
+@pytest.mark.parametrize("ct,cols", [(32, list(range(32))), (7, [6, 0, 3, 5]), (3, [2, 1])])
+def test_wide_fma_within_tolerance(ctx_fma, ct, cols):
+    rng = np.random.default_rng(40 + ct)
+    raw = synth_raw(rng, 25000, ct)
+    pos = rng.integers(100, 25100, size=61)  # includes zero-padded tails past the end
+    got = ctx_fma.process_recording(raw, ct, cols, [0.1] * len(cols), pos)
+    want = oracle.process_recording(raw, cols, [0.1] * len(cols), pos)
+    assert got.shape == (61, 16 * len(cols))
+    nan = np.isnan(want)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.max(np.abs(got[~nan] - want[~nan])) <= FMA_TOL
