@@ -93,6 +93,9 @@ SIGNATURES = {
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
     "eegfx_dwt8_operator": (c_int, [c_void_p]),
+    "eegfx_process_recording_streamed": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32,
+                                                 c_void_p, c_void_p, c_int32, c_void_p, c_int64,
+                                                 c_void_p, c_int64]),
     "eegfx_odp_create": (c_int, [c_void_p, POINTER(c_char_p), c_int32, POINTER(c_void_p)]),
     "eegfx_odp_load_data": (c_int, [c_void_p]),
     "eegfx_odp_error": (c_char_p, [c_void_p]),

@@ -144,6 +144,26 @@ class Context:
                                             ptr(pos), n, ptr(out), mem))
         return out
 
+    def process_recording_streamed(self, raw, n_channels_total: int, cols, res, pos,
+                                   chunk_frames: int = 1 << 22, out=None):
+        """configs[4]: the fused path over a host-resident recording streamed to the device in
+        chunks (eegfx_process_recording_streamed); raw/pos/out are host (numpy) arrays."""
+        cols_a, res_a = self._sel(cols, res)
+        if _is_device(raw):
+            raise ValueError("process_recording_streamed takes a host recording")
+        raw = np.ascontiguousarray(raw)
+        fmt = _fmt(raw)
+        n_frames = raw.size // n_channels_total
+        pos = np.ascontiguousarray(pos, dtype=np.int64)
+        n = pos.size
+        C = len(cols_a)
+        if out is None:
+            out = np.empty((n, 16 * C), dtype=np.float64)
+        check(lib().eegfx_process_recording_streamed(
+            self.handle, ptr(raw), fmt, n_frames, n_channels_total, ptr(cols_a), ptr(res_a), C,
+            ptr(pos), n, ptr(out), int(chunk_frames)))
+        return out
+
     def synth_recording(self, dst, n_channels: int, seed: int) -> None:
         """Fills a device int16 tensor (n_frames x n_channels) with the synthetic recording."""
         if not _is_device(dst):

@@ -33,6 +33,8 @@ struct DevBuf {
   size_t cap = 0;
   void* get(size_t bytes) {
     if (bytes > cap) {
+      // the old buffer may still be read by work queued on any stream of this device
+      if (p) (void)hipDeviceSynchronize();
       if (p) (void)hipFree(p);
       p = nullptr;
       cap = 0;
@@ -619,6 +621,119 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
       HIP_CHECK(hipMemcpyAsync(features, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       HIP_CHECK(hipStreamSynchronize(ctx->stream));
     }
+  });
+}
+
+// Config 5 (BASELINE.json configs[4]): a long recording in host memory, streamed to the device in
+// chunks of `chunk_frames` frames.  Epochs are taken in position order; a chunk starts at the
+// first unprocessed epoch's baseline frame (pos - 100) and holds every following epoch whose
+// frames [pos-100, pos+687) fit (or reach past the recording end, which the kernels zero-pad), so
+// consecutive chunks overlap by at most one epoch span (787 frames) -- the halo.  Two device
+// chunk buffers and a copy stream overlap the H2D of chunk k+1 with the kernels of chunk k; a
+// pageable source is first copied into one of two pinned staging buffers on the calling thread
+// (that copy overlaps the device work of the previous chunk), a pinned source (hipHostMalloc /
+// registered) is copied directly.
+int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fmt,
+                                     int64_t n_frames, int32_t ct, const int32_t* cols,
+                                     const float* res, int32_t C, const int64_t* pos, int64_t n,
+                                     double* features, int64_t chunk_frames) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    if (fmt != EEGFX_INT_16 && fmt != EEGFX_IEEE_FLOAT_32) fail(EEGFX_EINVAL, "format %d", fmt);
+    if (n_frames < 0 || n < 0 || ct < 1) fail(EEGFX_EINVAL, "negative size");
+    if (n > 0 && (!raw || !pos || !features)) fail(EEGFX_EINVAL, "null buffer");
+    constexpr int64_t kSpan = EEGFX_PRESTIMULUS + EEGFX_DWT8_SKIP + EEGFX_DWT8_EPOCH_SIZE;  // 787
+    if (chunk_frames < kSpan)
+      fail(EEGFX_EINVAL, "chunk_frames %lld < one epoch span (%lld)", (long long)chunk_frames,
+           (long long)kSpan);
+    const ChanSel sel = make_sel(cols, res, C, ct);
+    check_positions(pos, n, n_frames);
+    if (n == 0) return;
+    ctx->activate();
+    const int64_t FB = (int64_t)ct * (fmt == EEGFX_INT_16 ? 2 : 4);
+    const int64_t F = (int64_t)C * EEGFX_DWT8_FEATURE_SIZE;
+    std::vector<int64_t> order((size_t)n);
+    for (int64_t i = 0; i < n; ++i) order[(size_t)i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t a, int64_t b) { return pos[a] < pos[b]; });
+    std::vector<int64_t> spos((size_t)n);
+    for (int64_t i = 0; i < n; ++i) spos[(size_t)i] = pos[order[(size_t)i]];
+    int64_t* d_pos = (int64_t*)ctx->pos.get(sizeof(int64_t) * (size_t)n);
+    HIP_CHECK(hipMemcpyAsync(d_pos, spos.data(), sizeof(int64_t) * (size_t)n,
+                             hipMemcpyHostToDevice, ctx->stream));
+    double* d_out = (double*)ctx->out.get(sizeof(double) * (size_t)(n * F));
+    (void)ctx->fused.get(fused_scratch_bytes(n, C));  // every chunk's baselines fit: no realloc
+    // chunk buffers: 64 B front pad (the kernels round the first quad down by < 16 B) + data
+    // (rounded to 256 B so the second buffer is as aligned as the first: the kernels read
+    // 16-byte quads relative to `raw`)
+    const size_t cbytes = ((size_t)(chunk_frames * FB) + 128 + 255) & ~(size_t)255;
+    uint8_t* dbuf = (uint8_t*)ctx->raw.get(2 * cbytes);
+    hipPointerAttribute_t attr;
+    const bool pinned = hipPointerGetAttributes(&attr, raw) == hipSuccess &&
+                        attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // a pageable pointer can leave an error behind
+    void* pin[2] = {nullptr, nullptr};
+    hipStream_t cs = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    auto cleanup = [&] {
+      for (int b = 0; b < 2; ++b) {
+        if (pin[b]) (void)hipHostFree(pin[b]);
+        if (copied[b]) (void)hipEventDestroy(copied[b]);
+        if (done[b]) (void)hipEventDestroy(done[b]);
+      }
+      if (cs) (void)hipStreamDestroy(cs);
+    };
+    try {
+      HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        HIP_CHECK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+        if (!pinned) HIP_CHECK(hipHostMalloc(&pin[b], cbytes, hipHostMallocDefault));
+      }
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));  // d_pos uploaded; buffers idle
+      int64_t i = 0, k = 0;
+      while (i < n) {
+        const int b = (int)(k & 1);
+        const int64_t lo = spos[(size_t)i] - EEGFX_PRESTIMULUS;
+        const int64_t hi = std::min(lo + chunk_frames, n_frames);
+        int64_t j = i;
+        while (j < n && (spos[(size_t)j] - EEGFX_PRESTIMULUS + kSpan <= hi || hi == n_frames)) ++j;
+        const int64_t Lb = (lo * FB) & ~(int64_t)15, Hb = hi * FB;
+        const size_t bytes = Hb > Lb ? (size_t)(Hb - Lb) : 0;
+        uint8_t* dst = dbuf + (size_t)b * cbytes + 64;
+        if (k >= 2) HIP_CHECK(hipStreamWaitEvent(cs, done[b], 0));  // kernels of chunk k-2 done
+        const uint8_t* src = (const uint8_t*)raw + Lb;
+        if (!pinned) {
+          if (k >= 2) HIP_CHECK(hipEventSynchronize(copied[b]));  // staging b drained
+          if (bytes) memcpy(pin[b], src, bytes);
+          src = (const uint8_t*)pin[b];
+        }
+        if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs));
+        HIP_CHECK(hipEventRecord(copied[b], cs));
+        HIP_CHECK(hipStreamWaitEvent(ctx->stream, copied[b], 0));
+        // frame f of the recording lives at raw_dev + f*FB for lo <= f < hi (pointer arithmetic
+        // only: nothing below dst is ever read)
+        const uint8_t* raw_dev = dst - Lb;
+        run_features_from_raw(ctx, raw_dev, fmt, hi, ct, sel, C, d_pos + i, j - i,
+                              d_out + i * F);
+        HIP_CHECK(hipEventRecord(done[b], ctx->stream));
+        i = j;
+        ++k;
+      }
+      std::vector<double> sorted((size_t)(n * F));
+      HIP_CHECK(hipMemcpyAsync(sorted.data(), d_out, sizeof(double) * sorted.size(),
+                               hipMemcpyDeviceToHost, ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      for (int64_t r = 0; r < n; ++r)
+        memcpy(features + order[(size_t)r] * F, sorted.data() + r * F, sizeof(double) * (size_t)F);
+      HIP_CHECK(hipStreamSynchronize(cs));
+    } catch (...) {
+      (void)hipStreamSynchronize(ctx->stream);
+      if (cs) (void)hipStreamSynchronize(cs);
+      cleanup();
+      throw;
+    }
+    cleanup();
   });
 }
 

@@ -27,6 +27,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 namespace eegfx {
 namespace dev {
 
@@ -77,6 +79,14 @@ template <int N, bool FAST>
 __device__ __forceinline__ void lowpass(const double* in, double* out) {
 #pragma unroll
   for (int i = 0; i < N; ++i) out[i] = fir10<FAST, false>(in + 2 * i);
+}
+
+// The 16-byte quad a kernel reads in place of an out-of-range one (the value is discarded): the
+// last whole aligned quad of the recording.  Never offset 0: the streamed path
+// (eegfx_process_recording_streamed) passes a `raw` whose offset 0 lies before its chunk buffer.
+// Recordings under 16 bytes fall back to offset 0 of a resident (page-granular) allocation.
+__device__ __forceinline__ const uint8_t* safe_quad(const uint8_t* raw, int64_t nbytes) {
+  return nbytes >= 16 ? raw + ((nbytes & ~(int64_t)15) - 16) : raw;
 }
 
 // Orders LDS traffic of the lanes of one wave (DS ops of a wave execute in order; the fences

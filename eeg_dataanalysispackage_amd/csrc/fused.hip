@@ -99,7 +99,7 @@ __device__ __forceinline__ u32x4_a4 load16(const uint8_t* __restrict__ raw, int6
 __device__ __forceinline__ u32x4_a4 load16_bulk(const uint8_t* __restrict__ raw, int64_t nbytes,
                                                 int64_t A, bool want) {
   const bool full = want && A >= 0 && A + 16 <= nbytes;
-  const u32x4_a4 v = *(const u32x4_a16*)(raw + (full ? A : 0));
+  const u32x4_a4 v = *(const u32x4_a16*)(full ? raw + A : safe_quad(raw, nbytes));
   const u32x4_a4 z = {0u, 0u, 0u, 0u};
   return full ? v : z;
 }
@@ -454,12 +454,12 @@ __device__ __forceinline__ const float* meta_base(const uint32_t* mring, int64_t
 // Lanes 0..4*kMetaT-1: positions (quad q of tile t = lane/4); lanes 16..16+2*C*kMetaT-1:
 // baselines.  Out-of-range quads read the first quad of the recording (discarded).
 template <int C>
-__device__ __forceinline__ void dma_meta_batch(const uint8_t* __restrict__ raw,
+__device__ __forceinline__ void dma_meta_batch(const uint8_t* __restrict__ safe,
                                                const int64_t* __restrict__ pos,
                                                const float* __restrict__ base, int64_t n,
                                                int64_t ntl, int64_t batch, uint32_t* dst, int lane) {
   static_assert(C == 3, "meta layout assumes 3 channels");
-  const uint8_t* src = raw;
+  const uint8_t* src = safe;
   if (lane < 4 * kMetaT) {
     const int64_t i = batch * kMetaT + lane / 4;
     const int64_t e = ((int64_t)blockIdx.x + i * gridDim.x) * kSub + 2 * (lane % 4);
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
       qoff[j] = i2 < G::EPQ ? kSegLen * G::FB * sg + 16 * q : 0;
     }
     for (int b0 = 0; b0 < 2; ++b0)  // meta of the first two batches
-      dma_meta_batch<C>(raw, pos, base, n, ntl, b0, mring + b0 * kMetaQ * 4, lane);
+      dma_meta_batch<C>(safe_quad(raw, nbytes), pos, base, n, ntl, b0, mring + b0 * kMetaQ * 4, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int64_t i = 0; i < ntl && ok; ++i) {
       const int g = (int)(i % G_);
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
 #pragma unroll
       for (int e = 0; e < kSub; ++e) B[e] = e0 + e < n ? (mp[e] + 175) * G::FB : 0;
       if (batch_start)  // meta of batch i/kMetaT + 2
-        dma_meta_batch<C>(raw, pos, base, n, ntl, i / kMetaT + 2,
+        dma_meta_batch<C>(safe_quad(raw, nbytes), pos, base, n, ntl, i / kMetaT + 2,
                           mring + ((i / kMetaT + 2) % kMetaR) * kMetaQ * 4, lane);
       uint32_t* wn = win[g];
       if (e0 + kSub <= n && !tile_late<CT>(B, nbytes)) {
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
           const int sg = i2 / G::SEGQ, q = i2 - sg * G::SEGQ;
           const int64_t A = (B[e] & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
           const bool okq = e0 + e < n && i2 < G::EPQ && A + 16 <= nbytes;
-          if constexpr (!(EEGFX_FUSED_ABLATION & 8)) dma16(raw + (okq ? A : 0), wn + e * E::ESTR_E + 256 * j);
+          if constexpr (!(EEGFX_FUSED_ABLATION & 8)) dma16(okq ? raw + A : safe_quad(raw, nbytes), wn + e * E::ESTR_E + 256 * j);
         }
       }
       if (pending) {  // the previous tile: exactly its successor's DMAs (+ one meta DMA) are newer

@@ -99,8 +99,7 @@ struct TileAddr {
 };
 
 // Meta DMA: pos[e0 .. e0+16) (8 quads) then base[e0*C .. (e0+16)*C) (C*4 quads) into meta.
-// Lanes past the arrays read the first quad of the recording (nbytes >= 16 is a launch
-// precondition; the value is discarded).
+// Lanes past the arrays read `raw` = the recording's safe_quad (value discarded).
 template <int C>
 __device__ __forceinline__ void dma_meta(const uint8_t* __restrict__ raw, const int64_t* __restrict__ pos,
                                          const float* __restrict__ base, int64_t n, int64_t e0,
@@ -108,7 +107,7 @@ __device__ __forceinline__ void dma_meta(const uint8_t* __restrict__ raw, const 
   const uint8_t* src;
   if (lane < 8) {
     const int64_t i = e0 + 2 * lane;  // quad = 2 positions
-    src = i + 1 < n ? (const uint8_t*)(pos + i) : raw;
+    src = i + 1 < n ? (const uint8_t*)(pos + i) : raw;  // raw: the caller's safe_quad
   } else if (lane < 8 + 4 * C) {
     const int64_t f = e0 * C + 4 * (lane - 8);  // quad = 4 floats
     src = f + 3 < n * C ? (const uint8_t*)(base + f) : raw;
@@ -163,7 +162,7 @@ __device__ __forceinline__ bool dma_chunk(const uint8_t* __restrict__ raw, int64
     const int64_t a = ta.src[i] < 0 ? -1 : ta.src[i] + (int64_t)G::CHB * j;
     const bool ok = a >= 0 && a + 16 <= nbytes;
     bad |= a >= 0 && !ok;
-    dma16(raw + (ok ? a : 0), slot + 1024 * i);
+    dma16(ok ? raw + a : safe_quad(raw, nbytes), slot + 1024 * i);
   }
   return bad;
 }
@@ -253,7 +252,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void mfma_window_kernel(
 
   // prologue: meta of the first tile, then its first kAhead chunks
   int mb = 0;
-  dma_meta<C>(raw, pos, base, n, tile * kTileE, meta_a, lane);
+  dma_meta<C>(safe_quad(raw, nbytes), pos, base, n, tile * kTileE, meta_a, lane);
   wait_vm<0>();
   meta_fixup<C>(pos, base, n, tile * kTileE, meta0, lane);
   TileAddr cur, nxt;
@@ -292,7 +291,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void mfma_window_kernel(
       else wait_vm<2 * G::NI>();
       uint8_t* slot = ring + (j % kRing) * G::SLOT;
       if (fix & (1u << j)) fix_chunk<CT>(raw, nbytes, cur, j, slot);
-      if (j == 2) dma_meta<C>(raw, pos, base, n, e0n, meta_a + (mb ^ 1) * kMetaB, lane);
+      if (j == 2) dma_meta<C>(safe_quad(raw, nbytes), pos, base, n, e0n, meta_a + (mb ^ 1) * kMetaB, lane);
       if (j == 5) {
         meta_fixup<C>(pos, base, n, e0n, meta_nxt, lane);
         tile_addr<CT>(meta_nxt, e0n, n, n_frames, lane, nxt);

@@ -171,6 +171,20 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
                             int32_t C, const int64_t* pos, int64_t n_epochs, double* features,
                             int mem);
 
+/* configs[4] -- long recordings streamed from host memory: raw (host, n_frames x
+ * n_channels_total samples), pos and features are HOST arrays; the recording is moved to the device
+ * in chunks of chunk_frames frames (>= 787, the frames one epoch spans) on a copy stream that
+ * overlaps the kernels of the previous chunk (two device chunk buffers; pageable sources go through
+ * two pinned staging buffers, pinned sources are copied directly).  Positions may come in any
+ * order; features[i] belongs to pos[i].  Results equal eegfx_process_recording on the whole
+ * recording (bit for bit under EEGFX_EXACT).  Replaces the whole-file readBinaryData decode of
+ * OffLineDataProvider.java:186-188 for recordings that are not kept resident. */
+int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fmt,
+                                     int64_t n_frames, int32_t n_channels_total,
+                                     const int32_t* cols, const float* res, int32_t C,
+                                     const int64_t* pos, int64_t n_epochs, double* features,
+                                     int64_t chunk_frames);
+
 /* The fe=dwt-8 window transform as a matrix (host only, no device): M[16][512] row-major with
  * coefficient r of WaveletTransform's first 16 (a6[0..7] ++ d6[0..7], before normalisation)
  * = sum_k M[r][k] * epoch[c][175 + k].  This is the operator EEGFX_MFMA applies on the FP64

@@ -245,3 +245,32 @@ def test_wide_fma_within_tolerance(ctx_fma, ct, cols):
     nan = np.isnan(want)
     assert np.array_equal(np.isnan(got), nan)
     assert np.max(np.abs(got[~nan] - want[~nan])) <= FMA_TOL
+
+
+# ---- configs[4]: long recordings streamed from host memory in chunks -------------------------
+@pytest.mark.parametrize("chunk", [787, 1000, 4099, 1 << 20])
+def test_streamed_equals_resident(ctx, chunk):
+    rng = np.random.default_rng(chunk)
+    nf = 60000
+    raw = synth_raw(rng, nf, 3)
+    pos = rng.integers(100, nf + 100, size=400)  # unsorted, overlapping, tails past the end
+    pos[:3] = [100, nf + 100, nf - 50]
+    got = ctx.process_recording_streamed(raw, 3, [0, 1, 2], [0.1] * 3, pos, chunk_frames=chunk)
+    assert eq(got, ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, pos))
+    assert eq(got, oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos))
+
+
+def test_streamed_pinned_source_and_wide_layout(ctx_fma):
+    import torch
+    rng = np.random.default_rng(77)
+    nf, ct = 40000, 8
+    pinned = torch.empty((nf, ct), dtype=torch.int16, pin_memory=True)
+    pinned.numpy()[:] = synth_raw(rng, nf, ct)
+    raw = pinned.numpy()
+    pos = np.sort(rng.integers(100, nf, size=300))
+    cols = [7, 1, 4, 0, 2]
+    got = ctx_fma.process_recording_streamed(raw, ct, cols, [0.1] * 5, pos, chunk_frames=3000)
+    want = oracle.process_recording(raw, cols, [0.1] * 5, pos)
+    assert np.max(np.abs(got - want)) <= FMA_TOL
+    with pytest.raises(fx.EegfxError):
+        ctx_fma.process_recording_streamed(raw, ct, cols, [0.1] * 5, pos, chunk_frames=500)
