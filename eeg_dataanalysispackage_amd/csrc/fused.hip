@@ -186,9 +186,34 @@ __device__ __forceinline__ void decode_pairs(const int16_t (&xr)[kIn], float r, 
 // sub-tile, executed by one wave: lane e < ne folds Math.pow(f, 2) over row e in index order
 // (the 8 dependent chains run side by side), then the 64 lanes divide and store the rows
 // (coalesced 16-byte stores).  `norm` is an 8-double LDS scratch owned by the calling wave.
-template <int F>
+template <int F, bool FAST = false>
 __device__ __forceinline__ void normalise_store(const double* fb, double* norm, double* o, int ne,
                                                 int lane) {
+  if constexpr (FAST && F % 16 == 0) {
+    // FMA contract (1e-9): the 8 lanes of an epoch each square-sum F/8 features, a 3-step
+    // butterfly completes the row sum, and the row is scaled by one reciprocal (x * (1/s) is
+    // within 1 ulp of x / s; an all-zero row still gives NaN = 0 * inf).
+    constexpr int P = F / 8;
+    const int e = lane >> 3, p = lane & 7;
+    double v[P];
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      v[i] = e < ne ? fb[e * F + p * P + i] : 0.0;
+      acc = __builtin_fma(v[i], v[i], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    const double inv = 1.0 / sqrt(acc);
+    if (e < ne) {
+#pragma unroll
+      for (int i = 0; i < P; i += 2)
+        *(double2*)(o + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
+    }
+    (void)norm;
+    return;
+  }
   if (lane < ne) {
     double acc = 0.0;
 #pragma unroll 16
@@ -356,10 +381,144 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     __syncthreads();  // (B) features(kk) and window(kk+1) complete
     // normalisation: one wave (rotating over the sub-tiles of the workgroup); lanes 0..7 run the
     // 8 sequential sums of squares side by side, then all 64 lanes divide and store.
-    if (w == kk % C) normalise_store<F>(fb, norm, out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
+    if (w == kk % C) normalise_store<F, FAST>(fb, norm, out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
   }
 }
 
+
+// ================================================================================================
+// window_p_kernel -- window_kernel's sub-tile computation in a persistent workgroup with the next
+// sub-tile's window in flight during the filter bank.  window_kernel's one-shot workgroups pay two
+// dependent memory round trips before any arithmetic (marker positions, then the window DMA);
+// here the positions of sub-tile i+1 are in LDS before sub-tile i starts (loaded two iterations
+// ahead into a register) and its LDS-DMA is issued right after the current window has been copied
+// to registers (barrier A), into the same single window buffer -- the same LDS (32 KB) and VGPR
+// budget as window_kernel, so the same 5 workgroups per CU stay resident.
+template <int CT, int C>
+__device__ __forceinline__ bool dma_issue_b(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                            const int64_t* wbB, uint32_t* win, int w, int lane) {
+  using G = Geometry<CT>;
+  constexpr int PER_E = (G::EPQ + 63) / 64;
+  constexpr int NI = kSub * PER_E;
+  bool need_fix = false;
+#pragma unroll
+  for (int it = 0; it < (NI + C - 1) / C; ++it) {
+    const int m = w + it * C;
+    if (m < NI) {
+      const int e = m / PER_E, j = m - e * PER_E;
+      const int64_t B = wbB[e];
+      if (B >= 0) {
+        const int i = 64 * j + lane;
+        const int sg = i / G::SEGQ, q = i - sg * G::SEGQ;
+        const int64_t A = (B & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
+        if (i < G::EPQ) {
+          // perf-study bit 8: every DMA reads one L2-resident quad (LDS-write + issue cost only)
+          const int64_t src = (EEGFX_FUSED_ABLATION & 8) ? ((int64_t)(lane & 15) << 4) : A;
+          if (A + 16 <= nbytes) dma16(raw + src, win + e * G::ESTR + 256 * j);
+          else need_fix = true;
+        }
+      }
+    }
+  }
+  return need_fix;
+}
+
+template <int CT, int C>
+__device__ __forceinline__ void dma_fixup_b(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                            const int64_t* wbB, uint32_t* win, int w, int lane) {
+  using G = Geometry<CT>;
+  constexpr int PER_E = (G::EPQ + 63) / 64;
+  constexpr int NI = kSub * PER_E;
+  for (int m = w; m < NI; m += C) {
+    const int e = m / PER_E, j = m - e * PER_E;
+    const int i = 64 * j + lane;
+    const int64_t B = wbB[e];
+    if (B < 0 || i >= G::EPQ) continue;
+    const int sg = i / G::SEGQ, q = i - sg * G::SEGQ;
+    const int64_t A = (B & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
+    if (A + 16 > nbytes) lds_store4(win + e * G::ESTR + 256 * j + 4 * lane, load16(raw, nbytes, A));
+  }
+}
+
+template <int CT, int C, bool FAST, int MINW>
+__global__ __launch_bounds__(64 * C, MINW) void window_p_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
+    const float* __restrict__ base, int64_t n, double* __restrict__ out) {
+  using G = Geometry<CT>;
+  constexpr int F = C * 16;
+  __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
+  __shared__ __attribute__((aligned(16))) double feat[kSub * F];
+  __shared__ double norm[kSub];
+  __shared__ int64_t wbB[3][kSub];  // window byte offsets (-1: no epoch), ring over iterations
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int el = lane >> 3, s = lane & 7;
+  const int64_t nbytes = n_frames * G::FB;
+  const int col = sel.col[w];
+  const float r = sel.res[w];
+  const int64_t nsub = (n + kSub - 1) / kSub;
+  const int64_t stride = gridDim.x;
+  int64_t sub = blockIdx.x;
+  if (sub >= nsub) return;
+  auto wbyte = [&](int64_t sb) -> int64_t {  // wave 0 lanes 0..7: window byte offset of epoch lane
+    const int64_t e = sb * kSub + lane;
+    return sb < nsub && lane < kSub && e < n ? (pos[e] + 175) * G::FB : -1;
+  };
+  int64_t pq = 0;
+  if (w == 0) {
+    const int64_t b0 = wbyte(sub), b1 = wbyte(sub + stride);
+    if (lane < kSub) {
+      wbB[0][lane] = b0;
+      wbB[1][lane] = b1;
+    }
+    pq = wbyte(sub + 2 * stride);
+  }
+  float bcur = (sub * kSub + el < n) ? base[(sub * kSub + el) * C + w] : 0.0f;
+  __syncthreads();
+  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue_b<CT, C>(raw, nbytes, wbB[0], win, w, lane))
+    dma_fixup_b<CT, C>(raw, nbytes, wbB[0], win, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int64_t it = 0; sub < nsub; sub += stride, ++it) {  // uniform
+    const int64_t e0 = sub * kSub;
+    const int64_t nxt = sub + stride;
+    const int cur = (int)(it % 3), n1 = (int)((it + 1) % 3), n2 = (int)((it + 2) % 3);
+    // 1. this lane's 72 raw samples -> registers
+    const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + (int)(wbB[cur][el] & 15) + 2 * col;
+    const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
+    const int16_t* nx = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
+    int16_t xr[kIn];
+#pragma unroll
+    for (int k = 0; k < kSegLen; ++k) xr[k] = own[k * CT];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nx[k * CT];
+    const float b = bcur;
+    // 2. positions two sub-tiles ahead into the ring (loaded an iteration ago), the next load
+    if (w == 0) {
+      if (lane < kSub) wbB[n2][lane] = pq;
+      pq = wbyte(sub + 3 * stride);
+    }
+    __syncthreads();  // (A) the window is free; positions of sub-tiles it+1, it+2 are published
+    // 3. the next window streams in while the filter bank runs
+    const bool more = nxt < nsub;
+    bool need_fix = false;
+    if (more) {
+      bcur = (nxt * kSub + el < n) ? base[(nxt * kSub + el) * C + w] : 0.0f;
+      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue_b<CT, C>(raw, nbytes, wbB[n1], win, w, lane);
+    }
+    double x[kIn];
+    decode_pairs(xr, r, b, x);
+    double a6, d6;
+    dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
+    feat[el * F + w * 16 + s] = a6;
+    feat[el * F + w * 16 + 8 + s] = d6;
+    if (need_fix) dma_fixup_b<CT, C>(raw, nbytes, wbB[n1], win, w, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (B) features(it) and window(it+1) complete
+    if (w == (int)(it % C))
+      normalise_store<F, FAST>(feat, norm, out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
+  }
+}
 
 // ================================================================================================
 // engine_kernel -- the same sub-tile computation, decoupled from HBM by a loader wave.
@@ -627,7 +786,7 @@ __global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
 #pragma unroll
       for (int k = 0; k < C; ++k) ok = ok && spin_ge(&fdone[g][k], (uint32_t)(round + 1));
       if (!ok) return;
-      normalise_store<F>(fb, norm[g], out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
+      normalise_store<F, FAST>(fb, norm[g], out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
     }
   }
 }
@@ -705,6 +864,15 @@ bool engine_enabled() {
   return v;
 }
 
+// Persistent window kernel (EEGFX_WINDOW=p) vs the one-shot per-sub-tile one.
+bool window_p_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("EEGFX_WINDOW");
+    return e && e[0] == 'p';
+  }();
+  return v;
+}
+
 bool fused_supported(int fmt, int ct, int C, const double* out) {
   return fmt == 0 && ct == 3 && C == 3 && ((uintptr_t)out & 15) == 0;
 }
@@ -731,16 +899,34 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
                                const void* scratch, double* out) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
+  const float* bs = (const float*)scratch;
   if (engine_enabled() && n_frames * ct * 2 >= 16) {
     const char* gv = getenv("EEGFX_ENGINE_G");
     const int gsel = gv ? atoi(gv) : 3;
     if (fast)
-      return gsel == 4 ? launch_engine3<true, 4, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
-           : gsel == 2 ? launch_engine3<true, 3, 2>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
-                       : launch_engine3<true, 3, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
-    return gsel == 4 ? launch_engine3<false, 4, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
-         : gsel == 2 ? launch_engine3<false, 3, 2>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out)
-                     : launch_engine3<false, 3, 1>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
+      return gsel == 4 ? launch_engine3<true, 4, 1>(st, raw, n_frames, sel, pos, bs, n, out)
+                       : launch_engine3<true, 3, 1>(st, raw, n_frames, sel, pos, bs, n, out);
+    return gsel == 4 ? launch_engine3<false, 4, 1>(st, raw, n_frames, sel, pos, bs, n, out)
+                     : launch_engine3<false, 3, 1>(st, raw, n_frames, sel, pos, bs, n, out);
+  }
+  if (window_p_enabled()) {
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const int64_t nsub = (n + dev::kSub - 1) / dev::kSub;
+    const char* wv = getenv("EEGFX_WINDOW_WG");  // workgroups per CU (default 5: LDS-bound)
+    const int64_t per = wv ? atoi(wv) : 5;
+    const int64_t grid = nsub < per * (int64_t)cus ? nsub : per * (int64_t)cus;
+    const bool m3 = per <= 4;  // 4 WGs/CU fit 3 waves/SIMD: no spills at 168 VGPRs
+#define EEGFX_P(FA, MW)                                                                          \
+  hipLaunchKernelGGL((dev::window_p_kernel<3, 3, FA, MW>), dim3((unsigned)grid), dim3(192), 0, st, \
+                     (const uint8_t*)raw, n_frames, sel, pos, bs, n, out)
+    if (fast) { if (m3) EEGFX_P(true, 3); else EEGFX_P(true, 4); }
+    else { if (m3) EEGFX_P(false, 3); else EEGFX_P(false, 4); }
+#undef EEGFX_P
+    return hipGetLastError();
   }
   if (fast) launch_window3<true>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
   else launch_window3<false>(st, raw, n_frames, sel, pos, (const float*)scratch, n, out);
