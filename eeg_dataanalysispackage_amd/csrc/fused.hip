@@ -43,6 +43,12 @@
 #ifndef EEGFX_FUSED_ABLATION
 #define EEGFX_FUSED_ABLATION 0
 #endif
+// FMA-mode row store: 0 = each lane stores its own 6 normalised features (16-byte pieces 48 bytes
+// apart), 1 = rows staged back into LDS and stored as contiguous 1 KB wave stores, 2 = as 1 with
+// non-temporal stores.
+#ifndef EEGFX_STORE_MODE
+#define EEGFX_STORE_MODE 1
+#endif
 
 namespace eegfx {
 namespace dev {
@@ -206,10 +212,27 @@ __device__ __forceinline__ void normalise_store(const double* fb, double* norm, 
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
     const double inv = 1.0 / sqrt(acc);
-    if (e < ne) {
+    if constexpr (EEGFX_STORE_MODE == 0) {
+      if (e < ne) {
 #pragma unroll
-      for (int i = 0; i < P; i += 2)
-        *(double2*)(o + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
+        for (int i = 0; i < P; i += 2)
+          *(double2*)(o + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
+      }
+    } else {
+      double* fw = const_cast<double*>(fb);
+      if (e < ne) {
+#pragma unroll
+        for (int i = 0; i < P; i += 2)
+          *(double2*)(fw + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
+      }
+      wave_sync();
+      for (int i = 2 * lane; i < ne * F; i += 128) {
+        typedef double f64x2 __attribute__((ext_vector_type(2)));
+        const f64x2 q = *(const f64x2*)(fw + i);
+        if constexpr (EEGFX_STORE_MODE == 2) __builtin_nontemporal_store(q, (f64x2*)(o + i));
+        else *(f64x2*)(o + i) = q;
+      }
+      wave_sync();
     }
     (void)norm;
     return;
@@ -252,52 +275,103 @@ __device__ __forceinline__ void dma16(const uint8_t* src, uint32_t* lds_dst) {
       : "memory");
 }
 
-// Issues the LDS-DMA of one sub-tile's windows (wave w takes DMA instructions w, w+C, ...; every
-// guard is wave-uniform, so no VMEM op other than the DMAs is issued and nothing waits on them).
-// Returns whether some in-range quad of this wave could not be DMA'd (past the recording end).
+// Byte offset, from floor16(B_e), of the global quad that lands in LDS quad i of an epoch window
+// (segment i / SEGQ, quad i % SEGQ of that segment).  Depends on the lane only, so a kernel
+// computes it once per DMA row j (i = 64*j + lane) and every DMA of every epoch reuses it.
+template <int CT>
+__device__ __forceinline__ uint32_t quad_offset(int i) {
+  using G = Geometry<CT>;
+  const int sg = i / G::SEGQ;
+  return (uint32_t)(kSegLen * G::FB * sg + 16 * (i - G::SEGQ * sg));
+}
+
+template <int CT>
+struct DmaRows {
+  static constexpr int PER_E = (Geometry<CT>::EPQ + 63) / 64;  // 4 DMA rows per epoch window
+  uint32_t off[PER_E];
+  __device__ __forceinline__ explicit DmaRows(int lane) {
+#pragma unroll
+    for (int j = 0; j < PER_E; ++j) off[j] = quad_offset<CT>(64 * j + lane);
+  }
+};
+
+// global_load_lds_dwordx4 in its scalar-base form: lane l's 16 bytes at sbase + voff land at LDS
+// byte address lds_dst + 16*l.  The epoch's base is one SGPR pair and the lane offset a constant
+// VGPR, so a DMA costs no vector ALU work.
+__device__ __forceinline__ void dma16_s(const uint8_t* sbase, uint32_t voff, uint32_t* lds_dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(lds_ptr_t)lds_dst;
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "s"(lds), "v"(voff), "s"(sbase)
+      : "memory");
+}
+
+// Issues the LDS-DMA of one sub-tile's windows: wave w stages epochs w, w+C, w+2C, ... (every
+// DMA row of each).  The marker positions of those epochs are loaded (scalar) before the first
+// DMA, so the DMAs leave back to back; an epoch whose whole window lies inside the recording (a
+// scalar test) takes the unguarded path.  Returns whether some in-range quad of this lane could
+// not be DMA'd (the recording ends inside the window).
 template <int CT, int C>
 __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
                                           const int64_t* __restrict__ pos, int64_t n, int64_t e0,
-                                          uint32_t* win, int w, int lane) {
+                                          uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
-  constexpr int PER_E = (G::EPQ + 63) / 64;
-  constexpr int NI = kSub * PER_E;
+  constexpr int PER_E = DmaRows<CT>::PER_E;
+  constexpr int NE = (kSub + C - 1) / C;
+  constexpr int64_t kSpanB = kSegLen * G::FB * 7 + 16 * (G::SEGQ - 1) + 16;
+  int64_t Bq[NE];
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {  // unconditional (clamped) loads: one scalar round trip
+    const int64_t ei = e0 + (w + t * C < kSub ? w + t * C : kSub - 1);
+    Bq[t] = window_byte<CT>(pos, ei < n ? ei : n - 1) & ~(int64_t)15;
+  }
   bool need_fix = false;
 #pragma unroll
-  for (int it = 0; it < (NI + C - 1) / C; ++it) {
-    const int m = w + it * C;
-    if (m < NI) {
-      const int e = m / PER_E, j = m - e * PER_E;
-      if (e0 + e < n) {
-        const int64_t B = window_byte<CT>(pos, e0 + e);
-        const int i = 64 * j + lane;
-        const int sg = i / G::SEGQ, q = i - sg * G::SEGQ;
-        const int64_t A = (B & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
-        if (i < G::EPQ) {
-          if (A + 16 <= nbytes) dma16(raw + A, win + e * G::ESTR + 256 * j);
-          else need_fix = true;
-        }
+  for (int t = 0; t < NE; ++t) {
+    const int e = w + t * C;
+    if (e >= kSub || e0 + e >= n) continue;  // uniform
+    const uint8_t* sb = raw + Bq[t];
+    uint32_t* dst = win + e * G::ESTR;
+    if (Bq[t] + kSpanB <= nbytes) {
+#pragma unroll
+      for (int j = 0; j < PER_E; ++j)
+        if (64 * (j + 1) <= G::EPQ || 64 * j + lane < G::EPQ) dma16_s(sb, rows.off[j], dst + 256 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PER_E; ++j) {
+        if (64 * j + lane >= G::EPQ) continue;
+        if (Bq[t] + rows.off[j] + 16 <= nbytes) dma16_s(sb, rows.off[j], dst + 256 * j);
+        else need_fix = true;
       }
     }
   }
   return need_fix;
 }
 
-// Direct (non-DMA) fill of the quads dma_issue skipped: zero or partial quads at the recording end.
+// Direct (non-DMA) fill of the quads dma_issue skipped (same wave -> epoch mapping): zero or
+// partial quads at the recording end.
 template <int CT, int C>
 __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64_t nbytes,
                                           const int64_t* __restrict__ pos, int64_t n, int64_t e0,
-                                          uint32_t* win, int w, int lane) {
+                                          uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
-  constexpr int PER_E = (G::EPQ + 63) / 64;
-  constexpr int NI = kSub * PER_E;
-  for (int m = w; m < NI; m += C) {
-    const int e = m / PER_E, j = m - e * PER_E;
-    const int i = 64 * j + lane;
-    if (e0 + e >= n || i >= G::EPQ) continue;
-    const int sg = i / G::SEGQ, q = i - sg * G::SEGQ;
-    const int64_t A = (window_byte<CT>(pos, e0 + e) & ~(int64_t)15) + kSegLen * G::FB * sg + 16 * q;
-    if (A + 16 > nbytes) lds_store4(win + e * G::ESTR + 256 * j + 4 * lane, load16(raw, nbytes, A));
+  constexpr int PER_E = DmaRows<CT>::PER_E;
+  for (int e = w; e < kSub; e += C) {
+    if (e0 + e >= n) break;
+    const int64_t Bq = window_byte<CT>(pos, e0 + e) & ~(int64_t)15;
+#pragma unroll
+    for (int j = 0; j < PER_E; ++j) {
+      const int64_t A = Bq + rows.off[j];
+      if (64 * j + lane < G::EPQ && A + 16 > nbytes)
+        lds_store4(win + e * G::ESTR + 256 * j + 4 * lane, load16(raw, nbytes, A));
+    }
   }
 }
 
@@ -328,8 +402,9 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   if (w == 0 && lane < kSub)
     tdelta[0][lane] = first + lane < n ? (int)(window_byte<CT>(pos, first + lane) & 15) : 0;
   float bcur = (first + el < n) ? base[(first + el) * C + w] : 0.0f;
-  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane))
-    dma_fixup<CT, C>(raw, nbytes, pos, n, first, win, w, lane);
+  const DmaRows<CT> rows(lane);
+  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows))
+    dma_fixup<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
@@ -355,7 +430,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       if (w == 0 && lane < kSub)
         tdelta[(kk + 1) & 1][lane] = e1 + lane < n ? (int)(window_byte<CT>(pos, e1 + lane) & 15) : 0;
       bcur = (e1 + el < n) ? base[(e1 + el) * C + w] : 0.0f;
-      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane);
+      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane, rows);
     }
     double x[kIn];
     if constexpr (EEGFX_FUSED_ABLATION & 2) {
@@ -376,7 +451,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     double* fb = feat[kk & 1];
     fb[el * F + w * 16 + s] = a6;
     fb[el * F + w * 16 + 8 + s] = d6;
-    if (need_fix) dma_fixup<CT, C>(raw, nbytes, pos, n, e1, win, w, lane);
+    if (need_fix) dma_fixup<CT, C>(raw, nbytes, pos, n, e1, win, w, lane, rows);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (B) features(kk) and window(kk+1) complete
     // normalisation: one wave (rotating over the sub-tiles of the workgroup); lanes 0..7 run the

@@ -35,4 +35,10 @@ for NUM in ${NUMS:-fma exact}; do
     --kernel window_kernel --workload-key "fused_dwt8_c3_int16_1000000_$NUM" \
     --algorithmic-bytes 3476000000 --out "$OUT/traffic_$NUM.json"
 done
+cd "$ROOT"
+for WL in ${EXTRA:-c32 stream}; do
+  echo "== bench $WL"; date
+  timeout -k 10 400 python bench.py --workload $WL > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err" || { tail -30 "$OUT/bench_$WL.err"; exit 1; }
+  cat "$OUT/bench_$WL.json"
+done
 echo "== done"; date

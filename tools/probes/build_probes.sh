@@ -11,4 +11,7 @@ for A in 0 1 2 3 4 5 6 7 8 16 24; do
   $HIPCC $FL -DEEGFX_FUSED_ABLATION=$A window_probe.hip -o window_probe_$A &
 done
 for p in fp64_probe cascade_probe mem_probe; do $HIPCC $FL $p.hip -o $p & done
+for M in 1 2; do
+  $HIPCC $FL -DEEGFX_STORE_MODE=$M window_probe.hip -o window_probe_s$M &
+done
 wait
