@@ -51,8 +51,9 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed steps; ~50 ms of sustained load brings the clocks to their steady (power-capped) state")
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
     ap.add_argument("--workload", choices=["c3", "c32", "stream"], default="c3",
                     help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "

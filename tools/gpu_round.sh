@@ -24,7 +24,7 @@ cat "$OUT/bench.json"
 cd /tmp
 for NUM in ${NUMS:-fma exact}; do
   echo "== rocprofv3 kernel trace $NUM"; date
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$NUM" -o run -- python3 "$ROOT/bench.py" --numerics $NUM --steps 20 --warmup 3 --cpu-sample 0 --alt-steps 0 > "$OUT/trace_$NUM.log" 2>&1 || { tail -30 "$OUT/trace_$NUM.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$NUM" -o run -- python3 "$ROOT/bench.py" --numerics $NUM --cpu-sample 0 --alt-steps 0 > "$OUT/trace_$NUM.log" 2>&1 || { tail -30 "$OUT/trace_$NUM.log"; exit 1; }
   tail -1 "$OUT/trace_$NUM.log"
   find "$OUT/trace_$NUM" -name "*kernel_stats.csv" -exec cut -c1-200 {} \;
   for C in FETCH_SIZE WRITE_SIZE; do

@@ -3,9 +3,19 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../../eeg_dataanalysispackage_amd/csrc/fused.hip"
+
+__global__ void fill_random(uint32_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    p[i] = (uint32_t)z & 0x0FFF0FFFu;  // two int16 samples in [0, 4096)
+  }
+}
 
 int main() {
   const int64_t n = 1000000, nf = 1000 * n + 2000;
@@ -17,7 +27,8 @@ int main() {
   (void)hipMalloc(&pos, n * 8);
   (void)hipMalloc(&base, n * 12);
   (void)hipMalloc(&out, n * 48 * 8);
-  (void)hipMemset(raw, 3, nf * 6);
+  if (getenv("PROBE_RANDOM")) fill_random<<<4096, 256>>>((uint32_t*)raw, nf * 6 / 4);
+  else (void)hipMemset(raw, 3, nf * 6);
   std::vector<int64_t> hp(n);
   for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + 1000 * i;
   (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
@@ -29,13 +40,15 @@ int main() {
   (void)hipEventCreate(&b);
   for (int r = 0; r < 2; ++r)
     (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, true, base, out);
+  const char* it = getenv("PROBE_ITERS");
+  const int iters = it ? atoi(it) : 10;
   (void)hipEventRecord(a);
-  for (int r = 0; r < 10; ++r)
+  for (int r = 0; r < iters; ++r)
     (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, true, base, out);
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms;
   (void)hipEventElapsedTime(&ms, a, b);
-  printf("window ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, ms / 10);
+  printf("window ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, ms / iters);
   return 0;
 }
