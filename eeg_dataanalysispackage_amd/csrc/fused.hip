@@ -37,6 +37,7 @@
 
 #include "dwt8.h"
 #include "launch.h"
+#include "lds_dma.h"
 
 // Perf-study builds only (tools/probes/window_probe.hip): bit 0 drops the window DMA (and its
 // waits), bit 1 the LDS reads + decode, bit 2 the filter bank; the library is built with 0.
@@ -48,6 +49,11 @@
 // non-temporal stores.
 #ifndef EEGFX_STORE_MODE
 #define EEGFX_STORE_MODE 1
+#endif
+// Level-0 halo: 0 = every lane decodes its 8 halo samples from LDS, 1 = lanes decode only their
+// 64 own samples and take the halo (8 doubles) from lane s+1 through ds_bpermute.
+#ifndef EEGFX_HALO0_SHFL
+#define EEGFX_HALO0_SHFL 0
 #endif
 
 namespace eegfx {
@@ -162,7 +168,6 @@ __global__ __launch_bounds__(64 * C) void baseline_kernel(
   if (e < nt) bout[(t0 + e) * C + c] = b / (float)kPre;
 }
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // Byte offset of sub-tile epoch e's window: B_e = (pos + 175) * FB; quads are fetched from
 // floor16(B_e) and the lanes fold (B_e & 15) into their read base.  e0 and e are wave-uniform,
@@ -176,11 +181,12 @@ __device__ __forceinline__ int64_t window_byte(const int64_t* __restrict__ pos, 
 // each one correctly rounded fp32 operation (DataProviderUtils.java:49-59, Baseline.java:39-41),
 // evaluated two samples at a time with packed fp32 math (v_pk_mul_f32 / v_pk_add_f32).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int N = kIn>
 __device__ __forceinline__ void decode_pairs(const int16_t (&xr)[kIn], float r, float b,
                                              double (&x)[kIn]) {
   const f32x2 rr = {r, r}, bb = {b, b};
 #pragma unroll
-  for (int k = 0; k < kIn; k += 2) {
+  for (int k = 0; k < N; k += 2) {
     const f32x2 v = {(float)xr[k], (float)xr[k + 1]};
     const f32x2 y = v * rr - bb;
     x[k] = (double)y.x;
@@ -295,24 +301,6 @@ struct DmaRows {
   }
 };
 
-// global_load_lds_dwordx4 in its scalar-base form: lane l's 16 bytes at sbase + voff land at LDS
-// byte address lds_dst + 16*l.  The epoch's base is one SGPR pair and the lane offset a constant
-// VGPR, so a DMA costs no vector ALU work.
-__device__ __forceinline__ void dma16_s(const uint8_t* sbase, uint32_t voff, uint32_t* lds_dst) {
-  const uint32_t lds = (uint32_t)(uintptr_t)(lds_ptr_t)lds_dst;
-  uint32_t saved;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, %3\n\t"
-      "s_nop 0\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(saved)
-      : "s"(lds), "v"(voff), "s"(sbase)
-      : "memory");
-}
-
 // Issues the LDS-DMA of one sub-tile's windows: wave w stages epochs w, w+C, w+2C, ... (every
 // DMA row of each).  The marker positions of those epochs are loaded (scalar) before the first
 // DMA, so the DMAs leave back to back; an epoch whose whole window lies inside the recording (a
@@ -418,8 +406,10 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     int16_t xr[kIn];
 #pragma unroll
     for (int k = 0; k < kSegLen; ++k) xr[k] = own[k * CT];
+    if constexpr (!EEGFX_HALO0_SHFL) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nxt[k * CT];
+      for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nxt[k * CT];
+    }
     const float b = bcur;
     __syncthreads();  // (A) every lane holds its samples: the window is free
     // 2. the next sub-tile streams into the window while the filter bank runs
@@ -436,6 +426,9 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     if constexpr (EEGFX_FUSED_ABLATION & 2) {
 #pragma unroll
       for (int k = 0; k < kIn; ++k) x[k] = (double)b + k;
+    } else if constexpr (EEGFX_HALO0_SHFL) {
+      decode_pairs<kSegLen>(xr, r, b, x);
+      halo_shuffle<kSegLen>(x, lane & ~7, s);
     } else {
       decode_pairs(xr, r, b, x);
     }

@@ -21,6 +21,7 @@
 
 #include "dwt8.h"
 #include "launch.h"
+#include "lds_dma.h"
 
 namespace eegfx {
 namespace dev {
@@ -28,25 +29,76 @@ namespace dev {
 typedef uint32_t wq_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t wq_a16 __attribute__((ext_vector_type(4), aligned(16)));
 
+// The pre-stimulus frames [pos-100, pos) of EB epochs are staged in LDS by LDS-DMA (block m at
+// m*BSTQ quads: the block's quads are contiguous in the recording, and the +1 quad of stride skews
+// consecutive blocks by 4 banks), then lane (epoch, selected channel) folds its 100 samples from
+// LDS.  Quads outside the recording are staged as zeros, which is the reference's zero padding
+// for the fold (a padded +0.0f adds nothing, and the running sum is never -0.0f).
 template <typename T>
-__global__ __launch_bounds__(256) void baseline_any_kernel(const T* __restrict__ raw, int64_t n_frames,
-                                                           int ct, ChanSel sel, int C,
-                                                           const int64_t* __restrict__ pos,
-                                                           int64_t n, float* __restrict__ bout) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n * C) return;
-  const int64_t e = idx / C;
-  const int c = (int)(idx - e * C);
-  const int64_t lo = pos[e] - kPre;
-  const int col = sel.col[c];
+__global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __restrict__ raw,
+                                                           int64_t n_frames, int ct, ChanSel sel,
+                                                           int C, const int64_t* __restrict__ pos,
+                                                           int64_t n, int EB, int BSTQ,
+                                                           float* __restrict__ bout) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ int64_t sB[256];
+  const int FB = ct * (int)sizeof(T);
+  const int64_t nbytes = n_frames * FB;
+  const int64_t e0 = (int64_t)blockIdx.x * EB;
+  const int ne = (n - e0) < EB ? (int)(n - e0) : EB;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nw = blockDim.x / 64;
+  const int NQ = BSTQ - 1;  // quads staged per epoch
+  const int rows = (NQ + 63) / 64;
+  if (tid < ne) sB[tid] = (pos[e0 + tid] - kPre) * FB;
+  __syncthreads();
+  int m = 0, j = w;
+  while (j >= rows) { j -= rows; ++m; }
+  int mc = -1;
+  int64_t Bq = 0;
+  bool full = true;
+  for (; m < ne;) {
+    if (m != mc) {  // uniform
+      mc = m;
+      const int64_t v = sB[m] & ~(int64_t)15;  // same address in every lane: make it an SGPR pair
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+      Bq = (int64_t)(((uint64_t)hi << 32) | lo);
+      full = Bq >= 0 && Bq + 16 * NQ <= nbytes;
+    }
+    const int q = 64 * j + lane;
+    uint8_t* dst = smem + ((size_t)m * BSTQ + 64 * j) * 16;
+    if (q < NQ) {
+      const int64_t A = Bq + 16 * q;
+      if (full || (A >= 0 && A + 16 <= nbytes)) {
+        dma16_s(raw + Bq, (uint32_t)(16 * q), dst);
+      } else {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (A + 16 > 0 && A < nbytes) {  // the recording starts or ends inside this quad
+          uint32_t t[4] = {0u, 0u, 0u, 0u};
+          for (int k = 0; k < 4; ++k) {
+            const int64_t a = A + 4 * k;
+            if (a >= 0 && a + 4 <= nbytes) t[k] = *(const uint32_t*)(raw + a);
+            else if (a >= 0 && a + 2 <= nbytes) t[k] = *(const uint16_t*)(raw + a);
+          }
+          v = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        *(uint4*)(dst + 16 * lane) = v;
+      }
+    }
+    j += nw;
+    while (j >= rows) { j -= rows; ++m; }
+  }
+  dma_drain();
+  __syncthreads();
+  if (tid >= ne * C) return;
+  const int me = tid / C, c = tid - me * C;
+  const uint8_t* blk = smem + (size_t)me * BSTQ * 16 + (int)(sB[me] & 15) + sel.col[c] * (int)sizeof(T);
   const float r = sel.res[c];
   float b = 0.0f;
-  for (int i = 0; i < kPre; ++i) {
-    const int64_t f = lo + i;
-    const float v = (f >= 0 && f < n_frames) ? (float)raw[f * ct + col] * r : 0.0f;
-    b = b + v;
-  }
-  bout[idx] = b / (float)kPre;
+#pragma unroll 10
+  for (int i = 0; i < kPre; ++i) b = b + (float)*(const T*)(blk + i * FB) * r;
+  bout[(e0 + me) * C + c] = b / (float)kPre;
 }
 
 // One 16-byte quad of the recording at byte offset A (16-aligned), zero past the end.
@@ -86,21 +138,45 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   uint8_t* win = smem;
   double* feat = (double*)(smem + (size_t)EPW * EQ * 16);
   double* norm = feat + EPW * F;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t e0 = (int64_t)blockIdx.x * EPW;
   const int ne = (n - e0) < EPW ? (int)(n - e0) : EPW;
   const int64_t nbytes = n_frames * FB;
 
-  // stage the windows: quad i of epoch m = global quad floor16(B_m) + 64*FB*(i/SEGQ) + 16*(i%SEGQ)
-  for (int i = tid; i < ne * EQ; i += blockDim.x) {
-    const int m = i / EQ, iq = i - m * EQ;
-    const int sg = iq / SEGQ, q = iq - sg * SEGQ;
-    const int64_t B = (pos[e0 + m] + 175) * FB;
-    const int64_t A = (B & ~(int64_t)15) + (int64_t)64 * FB * sg + 16 * q;
-    const wq_a4 v = wide_load16(raw, nbytes, A);
-    uint32_t* d = (uint32_t*)(win + (size_t)i * 16);
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  // stage the windows: quad i of epoch m = global quad floor16(B_m) + 64*FB*(i/SEGQ) + 16*(i%SEGQ),
+  // by LDS-DMA rows of 64 quads (wave w takes rows w, w+4, ...): one SGPR base per epoch, the
+  // lane's quad offset from a float reciprocal (exact: i < 2^16, SEGQ < 2^12).  Quads the recording
+  // ends inside are filled directly.
+  const int nw = blockDim.x / 64;
+  const int nrows = (EQ + 63) / 64;
+  const float inv_segq = 1.0f / (float)SEGQ;
+  int64_t Bq[EPW];
+#pragma unroll
+  for (int m = 0; m < EPW; ++m)
+    Bq[m] = (((pos[e0 + (m < ne ? m : 0)] + 175) * FB) & ~(int64_t)15);
+  const int64_t span = (int64_t)64 * FB * 7 + 16 * SEGQ;
+#pragma unroll
+  for (int m = 0; m < EPW; ++m) {
+    if (m >= ne) break;  // uniform
+    const uint8_t* sb = raw + Bq[m];
+    const bool full = Bq[m] + span <= nbytes;
+    for (int j = w; j < nrows; j += nw) {
+      const int i = 64 * j + lane;
+      const int sg = (int)(((float)i + 0.5f) * inv_segq);
+      const uint32_t off = (uint32_t)(64 * FB * sg + 16 * (i - sg * SEGQ));
+      uint8_t* dst = win + ((size_t)m * EQ + 64 * j) * 16;
+      if (i < EQ) {
+        if (full || Bq[m] + off + 16 <= nbytes) {
+          dma16_s(sb, off, dst);
+        } else {
+          const wq_a4 v = wide_load16(raw, nbytes, Bq[m] + off);
+          uint32_t* d = (uint32_t*)(dst + 16 * lane);
+          d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+      }
+    }
   }
+  dma_drain();
   __syncthreads();
 
   // filter bank: signal = (epoch m, channel c), 8 per wave per pass
@@ -187,13 +263,18 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                                void* scratch) {
   if (n == 0) return hipSuccess;
-  const dim3 grid((unsigned)((n * C + 255) / 256));
+  const int FB = ct * (fmt == 0 ? 2 : 4);
+  const int BSTQ = (dev::kPre * FB + 15) / 16 + 2;  // staged quads + 1 quad of bank skew
+  int EB = 256 / C;  // lanes = (epoch, channel) pairs (<= 256 epochs: the sB table)
+  while (EB > 1 && (size_t)EB * BSTQ * 16 > 56 * 1024) --EB;
+  const size_t lds = (size_t)EB * BSTQ * 16;
+  const dim3 grid((unsigned)((n + EB - 1) / EB));
   if (fmt == 0)
-    hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), 0, st,
-                       (const int16_t*)raw, n_frames, ct, sel, C, pos, n, (float*)scratch);
+    hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), lds, st,
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
   else
-    hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), 0, st, (const float*)raw,
-                       n_frames, ct, sel, C, pos, n, (float*)scratch);
+    hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), lds, st,
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
   return hipGetLastError();
 }
 

@@ -156,6 +156,23 @@ def test_full_32_channel_montage(ctx):
     assert eq(got, oracle.process_recording(raw, cols, [0.1] * 32, pos))
 
 
+@pytest.mark.parametrize("ct,C", [(32, 32), (17, 5), (64, 2)])
+def test_wide_recording_edges_exact(ctx, ct, C):
+    """Any-layout kernels at the recording edges: the first legal marker (pos = 100: baseline from
+    frame 0), windows straddling the end (zero padding, partially staged quads) and an all-zero
+    epoch (pos - 100 == n_frames)."""
+    rng = np.random.default_rng(ct * 100 + C)
+    nf = 9000 + ct
+    raw = synth_raw(rng, nf, ct)
+    cols = list(rng.permutation(ct)[:C])
+    res = [0.1 + 0.01 * i for i in range(C)]
+    pos = np.concatenate([[100, 101, 102, 103], rng.integers(100, nf, size=30),
+                          np.arange(nf - 700, nf + 101, 37), [nf + 100]])
+    got = ctx.process_recording(raw, ct, cols, res, pos)
+    assert eq(got, oracle.process_recording(raw, cols, res, pos))
+    assert np.all(np.isnan(got[-1]))
+
+
 def test_ieee_float32_recording(ctx):
     rng = np.random.default_rng(11)
     raw = (rng.standard_normal((15000, 3)) * 50).astype(np.float32)
