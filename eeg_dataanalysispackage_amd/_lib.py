@@ -93,6 +93,15 @@ SIGNATURES = {
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
     "eegfx_dwt8_operator": (c_int, [c_void_p]),
+    "eegfx_shard_range": (c_int, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
+    "eegfx_comm_unique_id": (c_int, [c_void_p]),
+    "eegfx_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_void_p, POINTER(c_void_p)]),
+    "eegfx_comm_init_all": (c_int, [POINTER(c_void_p), c_int32, POINTER(c_void_p)]),
+    "eegfx_comm_rank": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    "eegfx_gather": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    "eegfx_group_start": (c_int, []),
+    "eegfx_group_end": (c_int, []),
+    "eegfx_comm_destroy": (c_int, [c_void_p]),
     "eegfx_process_recording_streamed": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32,
                                                  c_void_p, c_void_p, c_int32, c_void_p, c_int64,
                                                  c_void_p, c_int64]),

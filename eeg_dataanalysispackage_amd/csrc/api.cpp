@@ -449,6 +449,11 @@ struct eegfx_odp {
   }
 };
 
+namespace eegfx {
+int ctx_device(const eegfx_ctx* ctx) { return ctx->device; }
+void* ctx_stream(const eegfx_ctx* ctx) { return (void*)ctx->stream; }
+}  // namespace eegfx
+
 extern "C" {
 
 const char* eegfx_version(void) { return "eegfx 0.1.0 (gfx950)"; }

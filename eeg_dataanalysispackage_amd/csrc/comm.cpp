@@ -1,0 +1,156 @@
+// comm.cpp -- the multi-GPU boundary of the path (SURVEY.md 8b "eegfx_gather", 8e).
+//
+// After host marker planning every selected epoch is independent (OffLineDataProvider.java:
+// 200-265 is the only sequential state), so ranks take contiguous ranges of the selected-epoch
+// list and run the fused kernels on their range with no collective.  The one exchange is
+// assembling the per-rank feature rows in rank order -- the reference's getData() list order --
+// which eegfx_gather does with one RCCL broadcast per rank inside a group: shards may differ by a
+// row (eegfx_shard_range), and a rooted broadcast writes each shard straight into its final rows
+// of `out` with no padding or compaction pass.  RCCL runs over xGMI (peer-to-peer links) on an
+// MI355X node.  Normalisation is per row, so there is no statistic to all-reduce.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+using namespace eegfx;
+
+struct eegfx_comm {
+  ncclComm_t comm = nullptr;
+  eegfx_ctx* ctx = nullptr;
+  int world = 1, rank = 0;
+};
+
+namespace {
+
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) fail(EEGFX_EHIP, "%s: %s", what, ncclGetErrorString(r));
+}
+
+void shard(int64_t n, int world, int rank, int64_t* s, int64_t* e) {
+  const int64_t base = n / world, extra = n % world;
+  *s = rank * base + (rank < extra ? rank : extra);
+  *e = *s + base + (rank < extra ? 1 : 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int eegfx_shard_range(int64_t n, int32_t rank, int32_t world, int64_t* start, int64_t* end) {
+  return guarded([&] {
+    if (n < 0 || world < 1 || rank < 0 || rank >= world || !start || !end)
+      fail(EEGFX_EINVAL, "shard_range(n=%lld, rank=%d, world=%d)", (long long)n, rank, world);
+    shard(n, world, rank, start, end);
+  });
+}
+
+int eegfx_comm_unique_id(void* id) {
+  return guarded([&] {
+    if (!id) fail(EEGFX_EINVAL, "null id buffer");
+    static_assert(sizeof(ncclUniqueId) == EEGFX_COMM_ID_BYTES, "unique id size");
+    nccl_check(ncclGetUniqueId((ncclUniqueId*)id), "ncclGetUniqueId");
+  });
+}
+
+int eegfx_comm_create(eegfx_ctx* ctx, int32_t world, int32_t rank, const void* id,
+                      eegfx_comm** out) {
+  return guarded([&] {
+    if (!ctx || !id || !out) fail(EEGFX_EINVAL, "null argument");
+    if (world < 1 || rank < 0 || rank >= world) fail(EEGFX_EINVAL, "rank %d of %d", rank, world);
+    *out = nullptr;
+    auto* c = new eegfx_comm;
+    c->ctx = ctx;
+    c->world = world;
+    c->rank = rank;
+    if (hipSetDevice(ctx_device(ctx)) != hipSuccess) {
+      delete c;
+      fail(EEGFX_EHIP, "hipSetDevice(%d)", ctx_device(ctx));
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+    if (r != ncclSuccess) {
+      delete c;
+      nccl_check(r, "ncclCommInitRank");
+    }
+    *out = c;
+  });
+}
+
+int eegfx_comm_init_all(eegfx_ctx* const* ctxs, int32_t n, eegfx_comm** out) {
+  return guarded([&] {
+    if (!ctxs || !out || n < 1) fail(EEGFX_EINVAL, "init_all: %d contexts", n);
+    std::vector<int> dev((size_t)n);
+    for (int i = 0; i < n; ++i) {
+      if (!ctxs[i]) fail(EEGFX_EINVAL, "null context %d", i);
+      dev[(size_t)i] = ctx_device(ctxs[i]);
+      out[i] = nullptr;
+    }
+    std::vector<ncclComm_t> comms((size_t)n, nullptr);
+    nccl_check(ncclCommInitAll(comms.data(), n, dev.data()), "ncclCommInitAll");
+    for (int i = 0; i < n; ++i) {
+      auto* c = new eegfx_comm;
+      c->comm = comms[(size_t)i];
+      c->ctx = ctxs[i];
+      c->world = n;
+      c->rank = i;
+      out[i] = c;
+    }
+  });
+}
+
+int eegfx_comm_rank(const eegfx_comm* comm, int32_t* rank, int32_t* world) {
+  return guarded([&] {
+    if (!comm || !rank || !world) fail(EEGFX_EINVAL, "null argument");
+    *rank = comm->rank;
+    *world = comm->world;
+  });
+}
+
+int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t cols,
+                 double* out) {
+  return guarded([&] {
+    if (!comm || !out || n_total < 0 || cols < 1) fail(EEGFX_EINVAL, "gather arguments");
+    int64_t s = 0, e = 0;
+    shard(n_total, comm->world, comm->rank, &s, &e);
+    if (e > s && !local) fail(EEGFX_EINVAL, "null local rows");
+    if (hipSetDevice(ctx_device(comm->ctx)) != hipSuccess)
+      fail(EEGFX_EHIP, "hipSetDevice(%d)", ctx_device(comm->ctx));
+    const hipStream_t st = (hipStream_t)ctx_stream(comm->ctx);
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    ncclResult_t r = ncclSuccess;
+    for (int root = 0; root < comm->world && r == ncclSuccess; ++root) {
+      int64_t rs = 0, re = 0;
+      shard(n_total, comm->world, root, &rs, &re);
+      if (re == rs) continue;  // same decision on every rank
+      r = ncclBroadcast(root == comm->rank ? (const void*)local : nullptr, out + rs * cols,
+                        (size_t)((re - rs) * cols), ncclDouble, root, comm->comm, st);
+    }
+    const ncclResult_t g = ncclGroupEnd();
+    nccl_check(r, "ncclBroadcast");
+    nccl_check(g, "ncclGroupEnd");
+  });
+}
+
+int eegfx_group_start(void) {
+  return guarded([&] { nccl_check(ncclGroupStart(), "ncclGroupStart"); });
+}
+
+int eegfx_group_end(void) {
+  return guarded([&] { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); });
+}
+
+int eegfx_comm_destroy(eegfx_comm* comm) {
+  return guarded([&] {
+    if (!comm) return;
+    const ncclResult_t r = comm->comm ? ncclCommDestroy(comm->comm) : ncclSuccess;
+    delete comm;
+    nccl_check(r, "ncclCommDestroy");
+  });
+}
+
+}  // extern "C"

@@ -51,6 +51,10 @@ int guarded(F&& f) {
   }
 }
 
+// ---- context accessors for the other host sources (api.cpp) -----------------------------------
+int ctx_device(const eegfx_ctx* ctx);
+void* ctx_stream(const eegfx_ctx* ctx);  // the context's hipStream_t
+
 // ---- BrainVision reader (brainvision.cpp) ----------------------------------------------------
 struct Header {
   eegfx_header_info info;

@@ -10,7 +10,7 @@ the same code runs on gloo for the CPU tests.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Sequence, Tuple
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -41,3 +41,80 @@ def gather_features(local, n_total: int, group=None):
     dist.all_gather_into_tensor(full, padded, group=group)
     parts = [full[r * width: r * width + (e - s)] for r, (s, e) in enumerate(sizes)]
     return torch.cat(parts, dim=0)
+
+
+def native_shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """eegfx_shard_range through the C ABI (same partition as shard_range)."""
+    from ctypes import byref, c_int64
+    from ._lib import check, lib
+    s, e = c_int64(), c_int64()
+    check(lib().eegfx_shard_range(n, rank, world, byref(s), byref(e)))
+    return s.value, e.value
+
+
+class Comm:
+    """An RCCL communicator bound to a Context (eegfx_comm_* in include/eegfx.h).
+
+    ``Comm.unique_id()`` on rank 0, shipped to the other ranks out of band, then
+    ``Comm(ctx, world, rank, uid)`` on every rank; ``Comm.init_all(ctxs)`` for one process that
+    drives several devices.  ``gather(local, n_total)`` returns the [n_total][F] feature matrix in
+    rank order on every rank (device tensors, the context's stream)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, ctx, world: int, rank: int, uid: bytes, _handle=None):
+        from ctypes import byref, c_void_p, create_string_buffer
+        from ._lib import check, lib
+        self.ctx = ctx
+        if _handle is not None:
+            self.handle = _handle
+            return
+        if len(uid) != self.ID_BYTES:
+            raise ValueError(f"unique id must be {self.ID_BYTES} bytes")
+        h = c_void_p()
+        buf = create_string_buffer(bytes(uid), self.ID_BYTES)
+        check(lib().eegfx_comm_create(ctx.handle, world, rank, buf, byref(h)))
+        self.handle = h
+
+    @classmethod
+    def unique_id(cls) -> bytes:
+        from ctypes import create_string_buffer
+        from ._lib import check, lib
+        buf = create_string_buffer(cls.ID_BYTES)
+        check(lib().eegfx_comm_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def init_all(cls, ctxs: Sequence) -> list:
+        from ctypes import c_void_p
+        from ._lib import check, lib
+        n = len(ctxs)
+        hs = (c_void_p * n)(*[c.handle for c in ctxs])
+        out = (c_void_p * n)()
+        check(lib().eegfx_comm_init_all(hs, n, out))
+        return [cls(c, n, i, b"", _handle=c_void_p(out[i])) for i, c in enumerate(ctxs)]
+
+    def rank_world(self) -> Tuple[int, int]:
+        from ctypes import byref, c_int32
+        from ._lib import check, lib
+        r, w = c_int32(), c_int32()
+        check(lib().eegfx_comm_rank(self.handle, byref(r), byref(w)))
+        return r.value, w.value
+
+    def gather(self, local, n_total: int, out=None):
+        import torch
+        from ._lib import check, lib
+        _, world = self.rank_world()
+        cols = int(local.shape[1])
+        if out is None:
+            out = torch.empty((n_total, cols), dtype=torch.float64, device=local.device)
+        local = local.contiguous()
+        check(lib().eegfx_gather(self.handle, local.data_ptr() if local.numel() else None,
+                                 n_total, cols, out.data_ptr()))
+        return out
+
+    def close(self) -> None:
+        from ._lib import check, lib
+        if getattr(self, "handle", None):
+            h, self.handle = self.handle, None
+            check(lib().eegfx_comm_destroy(h))

@@ -185,6 +185,31 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
                                      const int64_t* pos, int64_t n_epochs, double* features,
                                      int64_t chunk_frames);
 
+/* ---- multi-GPU ------------------------------------------------------------
+ * Epochs shard by contiguous ranges of the selected-epoch list (eegfx_shard_range: balanced, the
+ * first n % world ranks take one more); each rank runs the fused path on its range with no
+ * collective; eegfx_gather then assembles the [n_total][cols] feature matrix in rank order (the
+ * reference's getData() order, OffLineDataProvider.java:370) on every rank, by one RCCL broadcast
+ * per rank inside a group (ragged shards land directly in their rows).  `local` and `out` are
+ * device pointers on the communicator's context device; the collective runs on that context's
+ * stream.  One communicator per (process, device): rank 0 creates the unique id and ships it to
+ * the other ranks out of band (e.g. a Spark broadcast variable); a single process that drives
+ * several devices (Spark local[*]) uses eegfx_comm_init_all and brackets its per-device gathers
+ * with eegfx_group_start / eegfx_group_end. */
+#define EEGFX_COMM_ID_BYTES 128
+typedef struct eegfx_comm eegfx_comm;
+int eegfx_shard_range(int64_t n, int32_t rank, int32_t world, int64_t* start, int64_t* end);
+int eegfx_comm_unique_id(void* id /* EEGFX_COMM_ID_BYTES */);
+int eegfx_comm_create(eegfx_ctx* ctx, int32_t world, int32_t rank, const void* id,
+                      eegfx_comm** out);
+int eegfx_comm_init_all(eegfx_ctx* const* ctxs, int32_t n, eegfx_comm** out /* n */);
+int eegfx_comm_rank(const eegfx_comm* comm, int32_t* rank, int32_t* world);
+int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t cols,
+                 double* out);
+int eegfx_group_start(void);
+int eegfx_group_end(void);
+int eegfx_comm_destroy(eegfx_comm* comm);
+
 /* The fe=dwt-8 window transform as a matrix (host only, no device): M[16][512] row-major with
  * coefficient r of WaveletTransform's first 16 (a6[0..7] ++ d6[0..7], before normalisation)
  * = sum_k M[r][k] * epoch[c][175 + k].  This is the operator EEGFX_MFMA applies on the FP64

@@ -25,6 +25,17 @@ def test_shard_range_partitions():
         shard_range(10, 2, 2)
 
 
+def test_native_shard_range_matches():
+    from eeg_dataanalysispackage_amd.sharding import native_shard_range
+    import eeg_dataanalysispackage_amd as fx
+    for n in (0, 1, 7, 64, 1_000_003, 64_000_000):
+        for world in (1, 2, 3, 8):
+            for r in range(world):
+                assert native_shard_range(n, r, world) == shard_range(n, r, world)
+    with pytest.raises(fx.EegfxError):
+        native_shard_range(10, 2, 2)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
