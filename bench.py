@@ -55,11 +55,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps; ~50 ms of sustained load brings the clocks to their steady (power-capped) state")
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
-    ap.add_argument("--workload", choices=["c3", "c32", "stream"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c32", "stream", "logreg"], default="c3",
                     help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "
                          "32-channel montage, every channel through the DWT, 512-dim); stream: "
                          "configs[4] (4 h recordings in pinned host memory, a marker every 100 ms, "
-                         "streamed to the device in chunks)")
+                         "streamed to the device in chunks); logreg: the downstream classifier "
+                         "(MLlib LogisticRegressionWithSGD, 100 full-batch iterations) on the 1M "
+                         "48-dim feature rows of c3")
     ap.add_argument("--chunk-frames", type=int, default=1 << 22, help="stream workload chunk")
     ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
@@ -112,6 +114,8 @@ def main():
 
     if args.workload == "stream":
         return bench_stream(args, rank, world, dev, dist if distributed else None)
+    if args.workload == "logreg":
+        return bench_logreg(args, rank, world, dev, dist if distributed else None)
     wl = WORKLOADS[args.workload]
     ct, C = wl["ct"], wl["C"]
     if args.workload == "c32" and args.epochs == 1_000_000:
@@ -323,6 +327,91 @@ def bench_stream(args, rank, world, dev, dist):
                           "bytes_per_step": nf * 6,
                           "note": "every frame crosses the host link once per step"},
         }), flush=True)
+    ctx.close()
+
+
+def bench_logreg(args, rank, world, dev, dist):
+    """LogisticRegressionClassifier's training (MLlib LogisticRegressionWith
+    SGD defaults: 100 iterations, step 1.0, regParam 0.01, full batch) on the device-resident
+    feature rows of the c3 workload.  A step = one whole training run; value = rows x iterations
+    per second; the roofline is the gradient pass, which reads the n x 48 rows + labels once per
+    iteration."""
+    import torch
+    import eeg_dataanalysispackage_amd as fx
+    from eeg_dataanalysispackage_amd import classification as clf
+    n = args.epochs
+    ctx = fx.Context(dev.index, numerics=args.numerics)
+    raw = torch.empty((FRAMES_PER_EPOCH * n + 2000, 3), dtype=torch.int16, device=dev)
+    ctx.synth_recording(raw, 3, SEED + rank)
+    pos = torch.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (n + 1), FRAMES_PER_EPOCH,
+                       dtype=torch.int64, device=dev)
+    X = ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, pos)
+    del raw
+    ctx.synchronize()
+    # labels: the sign of a fixed direction plus noise (deterministic), both classes present
+    g = torch.Generator(device=dev).manual_seed(SEED)
+    w0 = torch.randn(48, generator=g, device=dev, dtype=torch.float64)
+    y = ((X @ w0 + 0.1 * torch.randn(n, generator=g, device=dev, dtype=torch.float64)) > 0)
+    y = y.to(torch.float64).contiguous()
+    torch.cuda.synchronize(dev)
+    iters = clf.DEFAULT_NUM_ITERATIONS
+
+    def step():
+        return clf.sgd_train(ctx, X, y, iters, clf.DEFAULT_STEP_SIZE, clf.DEFAULT_REG_PARAM,
+                             clf.DEFAULT_MINI_BATCH_FRACTION, convergence_tol=0.0)
+
+    for _ in range(max(1, min(args.warmup, 5))):
+        w, it = step()
+    steps = max(1, min(args.steps, 20))
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w, it = step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    per_iter = elapsed / steps / it
+    bytes_iter = n * 48 * 8 + n * 8
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle import mllib_logreg as ref
+        k = min(n, 100_000)
+        Xh, yh = X[:k].cpu().numpy(), y[:k].cpu().numpy()
+        c0 = time.perf_counter()
+        wr, itr = ref.sgd_train(Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0)
+        cdt = time.perf_counter() - c0
+        wg, itg = clf.sgd_train(ctx, Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0)
+        cpu = {"value": round(k * itr / cdt, 1), "unit": "rows*iterations/s", "cores": 1,
+               "kind": "port",
+               "sample": f"first {k} rows, numpy restatement of MLlib 1.6.2 "
+                         f"LogisticRegressionWithSGD ({itr} iterations, one partition), "
+                         f"{cdt:.2f} s wall",
+               "gpu_parity_on_sample": bool(np.linalg.norm(wg - wr) <= 1e-9 * np.linalg.norm(wr))}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "logistic-regression SGD rows*iterations/s (MLlib LogisticRegressionWithSGD, "
+                      "full batch) on the dwt-8 feature rows",
+            "value": round(world * n * it * steps / elapsed, 1),
+            "unit": "rows*iterations/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "logreg: 100 iterations, step 1.0, regParam 0.01 over the c3 "
+                                   "feature rows (1M x 48 per GPU), labels from a fixed direction",
+                       "rows_per_gpu": n, "features": 48, "iterations": it},
+            "roofline": {"bound": "hbm", "achieved": round(bytes_iter / per_iter / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(bytes_iter / per_iter / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "lr_grad16_kernel + lr_update_kernel",
+                         "bytes_per_iteration": bytes_iter,
+                         "ms_per_iteration": round(per_iter * 1e3, 4)},
+            "cpu_baseline": cpu}), flush=True)
     ctx.close()
 
 

@@ -93,6 +93,11 @@ SIGNATURES = {
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
     "eegfx_dwt8_operator": (c_int, [c_void_p]),
+    "eegfx_logreg_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                       c_double, c_double, c_double, c_double, c_void_p,
+                                       POINTER(c_int32), c_int]),
+    "eegfx_logreg_predict": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_double,
+                                     c_double, c_void_p, c_int]),
     "eegfx_shard_range": (c_int, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     "eegfx_comm_unique_id": (c_int, [c_void_p]),
     "eegfx_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_void_p, POINTER(c_void_p)]),

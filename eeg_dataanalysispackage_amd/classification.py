@@ -1,0 +1,178 @@
+"""The downstream classifier of the train/test flow on the GPU.
+
+Mirrors ``Classification/LogisticRegressionClassifier`` (IClassifier) and
+``Utils/ClassificationStatistics`` of the reference: ``train(epochs, targets, fe)`` extracts the
+features of the epochs (one batched device call instead of the Spark map of :90) and fits Spark
+MLlib 1.6.2 ``LogisticRegressionWithSGD`` on the device (``eegfx_logreg_sgd_train``);
+``test(epochs, targets)`` predicts on the device and builds the statistics exactly as :117-141 do,
+including the reference's reading of the column-major confusion matrix (its "false positives"
+count actual-1 / predicted-0).  Model save/load (Spark model directories) is out of scope.
+"""
+from __future__ import annotations
+
+import math
+from ctypes import byref, c_int32
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from ._lib import EegfxError, check, lib, ptr
+from .context import Context, _is_device, _mem
+
+# LogisticRegressionWithSGD() defaults (MLlib 1.6.2) and GradientDescent's convergence tolerance
+DEFAULT_STEP_SIZE = 1.0
+DEFAULT_NUM_ITERATIONS = 100
+DEFAULT_REG_PARAM = 0.01
+DEFAULT_MINI_BATCH_FRACTION = 1.0
+CONVERGENCE_TOL = 0.001
+
+
+def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
+              step_size: float = DEFAULT_STEP_SIZE, reg_param: float = 0.0,
+              mini_batch_fraction: float = DEFAULT_MINI_BATCH_FRACTION,
+              convergence_tol: float = CONVERGENCE_TOL, initial_weights=None):
+    """Full-batch LogisticRegressionWithSGD on the device; returns (weights, iterations_run).
+    X (n x d float64, host numpy or device torch) and y (n labels 0/1) may live on either side."""
+    if _is_device(X) != _is_device(y):
+        raise ValueError("X and y must both be host or both be device arrays")
+    if not _is_device(X):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+    n, d = int(X.shape[0]), int(X.shape[1])
+    w = (np.zeros(d) if initial_weights is None
+         else np.array(initial_weights, dtype=np.float64).copy())
+    it = c_int32()
+    check(lib().eegfx_logreg_sgd_train(ctx.handle, ptr(X), ptr(y), n, d, int(num_iterations),
+                                       float(step_size), float(reg_param),
+                                       float(mini_batch_fraction), float(convergence_tol),
+                                       ptr(w), byref(it), _mem(X, y)))
+    return w, it.value
+
+
+def predict(ctx: Context, X, weights, intercept: float = 0.0,
+            threshold: Optional[float] = 0.5):
+    """LogisticRegressionModel.predict on the device: 0/1 per row, or the score when
+    ``threshold`` is None (clearThreshold)."""
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    n, d = int(X.shape[0]), int(X.shape[1])
+    if _is_device(X):
+        import torch
+        out = torch.empty(n, dtype=torch.float64, device=X.device)
+    else:
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        out = np.empty(n, dtype=np.float64)
+    t = math.nan if threshold is None else float(threshold)
+    check(lib().eegfx_logreg_predict(ctx.handle, ptr(X), n, d, ptr(w), float(intercept), t,
+                                     ptr(out), _mem(X, out)))
+    return out
+
+
+class ClassificationStatistics:
+    """Utils/ClassificationStatistics.java (the counters the classifiers report)."""
+
+    def __init__(self, truePositives: int = 0, trueNegatives: int = 0, falsePositives: int = 0,
+                 falseNegatives: int = 0):
+        self.truePositives = int(truePositives)
+        self.trueNegatives = int(trueNegatives)
+        self.falsePositives = int(falsePositives)
+        self.falseNegatives = int(falseNegatives)
+
+    def getNumberOfPatterns(self) -> int:
+        return self.truePositives + self.trueNegatives + self.falsePositives + self.falseNegatives
+
+    def calcAccuracy(self) -> float:
+        n = self.getNumberOfPatterns()
+        return (self.truePositives + self.trueNegatives) / n if n else math.nan
+
+    def as_tuple(self):
+        return (self.truePositives, self.trueNegatives, self.falsePositives, self.falseNegatives)
+
+    def __repr__(self) -> str:
+        return (f"Number of patterns: {self.getNumberOfPatterns()}\n"
+                f"True positives: {self.truePositives}\nTrue negatives: {self.trueNegatives}\n"
+                f"False positives: {self.falsePositives}\n"
+                f"False negatives: {self.falseNegatives}\n"
+                f"Accuracy: {self.calcAccuracy() * 100}%\n")
+
+
+def reference_statistics(predictions, labels) -> ClassificationStatistics:
+    """LogisticRegressionClassifier.test :129-137: MulticlassMetrics' confusion matrix (rows =
+    actual, columns = predicted, labels ascending) flattened column-major by toArray and read as
+    tn, fp, fn, tp = cm[0], cm[1], cm[2], cm[3].  With a single class present the matrix is 1x1
+    and the reference's cm[1] throws; so does this (IndexError)."""
+    p = np.asarray(predictions, dtype=np.float64)
+    a = np.asarray(labels, dtype=np.float64)
+    classes = sorted(set(a.tolist()) | set(p.tolist()))
+    k = len(classes)
+    cm = np.zeros((k, k), dtype=np.int64)
+    idx = {c: i for i, c in enumerate(classes)}
+    for ai, pi in zip(a.tolist(), p.tolist()):
+        cm[idx[ai], idx[pi]] += 1
+    flat = cm.flatten(order="F")
+    tn, fp, fn, tp = (int(flat[0]), int(flat[1]), int(flat[2]), int(flat[3]))
+    return ClassificationStatistics(tp, tn, fp, fn)
+
+
+class LogisticRegressionClassifier:
+    """IClassifier for train_clf=logreg (LogisticRegressionClassifier.java), GPU-resident."""
+
+    def __init__(self, context: Optional[Context] = None):
+        self._ctx = context
+        self.fe = None
+        self.config: Dict[str, str] = {}
+        self.weights: Optional[np.ndarray] = None
+        self.iterations_run = 0
+
+    @property
+    def context(self) -> Context:
+        if self._ctx is None:
+            self._ctx = Context(0)
+        return self._ctx
+
+    def setFeatureExtraction(self, fe) -> None:
+        self.fe = fe
+
+    def getFeatureExtraction(self):
+        return self.fe
+
+    def setConfig(self, config: Dict[str, str]) -> None:
+        self.config = dict(config)
+
+    def _features(self, epochs):
+        if self.fe is None:
+            raise ValueError("no feature extraction set")
+        ep = np.ascontiguousarray(np.asarray(epochs, dtype=np.float64))
+        return self.fe.extractFeaturesBatch(ep)
+
+    def train(self, epochs, targets: Sequence[float], fe) -> None:
+        """:85-114 -- the config_* keys select the static train(...) (regParam 0.0), otherwise
+        the default LogisticRegressionWithSGD().run (regParam 0.01)."""
+        self.fe = fe
+        X = self._features(epochs)
+        y = np.asarray(targets, dtype=np.float64)
+        c = self.config
+        if all(k in c for k in ("config_num_iterations", "config_step_size",
+                                "config_mini_batch_fraction")):
+            self.weights, self.iterations_run = sgd_train(
+                self.context, X, y, num_iterations=int(c["config_num_iterations"]),
+                step_size=float(c["config_step_size"]), reg_param=0.0,
+                mini_batch_fraction=float(c["config_mini_batch_fraction"]))
+        else:
+            self.weights, self.iterations_run = sgd_train(
+                self.context, X, y, DEFAULT_NUM_ITERATIONS, DEFAULT_STEP_SIZE, DEFAULT_REG_PARAM,
+                DEFAULT_MINI_BATCH_FRACTION)
+
+    def predict(self, features) -> np.ndarray:
+        if self.weights is None:
+            raise RuntimeError("The classifier has not been trained")  # IllegalStateException
+        return predict(self.context, features, self.weights)
+
+    def test(self, epochs, targets: Sequence[float]) -> ClassificationStatistics:
+        if self.weights is None:
+            raise RuntimeError("The classifier has not been trained")
+        pred = self.predict(self._features(epochs))
+        return reference_statistics(pred, targets)
+
+
+__all__ = ["ClassificationStatistics", "LogisticRegressionClassifier", "predict",
+           "reference_statistics", "sgd_train", "EegfxError"]

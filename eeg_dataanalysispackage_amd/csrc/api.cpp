@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <thread>
 #include <cstring>
 #include <memory>
@@ -103,6 +104,7 @@ struct eegfx_ctx {
   std::vector<int64_t> event_bytes;
   size_t n_timed = 0;
   DevBuf raw, pos, out, scratch, fused;
+  DevBuf lr_x, lr_y, lr_state, lr_part;  // logistic regression (eegfx_logreg_*)
   DevBuf mop;  // dwt-8 operator rows for EEGFX_MFMA (uploaded on first use)
   bool mop_ready = false;
 
@@ -782,6 +784,91 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       throw;
     }
     cleanup();
+  });
+}
+
+// the classifier of LogisticRegressionClassifier.java:85-114 on the GPU
+// (csrc/logreg.hip): MLlib 1.6.2 LogisticRegressionWithSGD, full batch.  miniBatchFraction < 1
+// samples each partition with Spark's own seeded Bernoulli sampler, which depends on Spark's
+// partitioning -- not reproducible outside Spark, so it is refused.
+int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
+                           int32_t num_iterations, double step_size, double reg_param,
+                           double mini_batch_fraction, double convergence_tol, double* weights,
+                           int32_t* iterations_run, int mem) {
+  return guarded([&] {
+    if (!ctx || !weights) fail(EEGFX_EINVAL, "null argument");
+    check_mem(mem);
+    if (n < 1) fail(EEGFX_EINVAL, "empty training set");  // GeneralizedLinearAlgorithm: first()
+    if (!X || !y) fail(EEGFX_EINVAL, "null X / y");
+    if (d < 1 || d > kLrMaxFeatures) fail(EEGFX_EINVAL, "d=%d outside [1, %d]", d, kLrMaxFeatures);
+    if (num_iterations < 0) fail(EEGFX_EINVAL, "num_iterations %d", num_iterations);
+    if (mini_batch_fraction != 1.0)
+      fail(EEGFX_ENOTSUP, "miniBatchFraction %g: only full-batch (1.0) gradient descent",
+           mini_batch_fraction);
+    ctx->activate();
+    const double* dX = X;
+    const double* dy = y;
+    if (mem == EEGFX_MEM_HOST) {
+      double* bx = (double*)ctx->lr_x.get(sizeof(double) * (size_t)(n * d));
+      double* by = (double*)ctx->lr_y.get(sizeof(double) * (size_t)n);
+      HIP_CHECK(hipMemcpyAsync(bx, X, sizeof(double) * (size_t)(n * d), hipMemcpyHostToDevice,
+                               ctx->stream));
+      HIP_CHECK(hipMemcpyAsync(by, y, sizeof(double) * (size_t)n, hipMemcpyHostToDevice,
+                               ctx->stream));
+      dX = bx;
+      dy = by;
+    }
+    const size_t sbytes = sizeof(LrState) + sizeof(double) * (size_t)d;
+    std::vector<uint8_t> hs(sbytes, 0);
+    LrState* h = (LrState*)hs.data();
+    h->converged = num_iterations == 0 ? 1 : 0;
+    memcpy(h->w, weights, sizeof(double) * (size_t)d);  // initial weights (zeros in MLlib)
+    LrState* st = (LrState*)ctx->lr_state.get(sbytes);
+    HIP_CHECK(hipMemcpyAsync(st, hs.data(), sbytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(launch_lr_validate(ctx->stream, dy, n, st));
+    const int G = lr_grid(n);
+    double* part = (double*)ctx->lr_part.get(sizeof(double) * (size_t)G * d);
+    for (int i = 0; i < num_iterations; ++i)
+      HIP_CHECK(launch_lr_iteration(ctx->stream, dX, dy, n, d, st, part, G, step_size, reg_param,
+                                    convergence_tol, num_iterations));
+    HIP_CHECK(hipMemcpyAsync(hs.data(), st, sbytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h->converged == 2) fail(EEGFX_EINVAL, "Input validation failed: labels must be 0.0 or 1.0");
+    memcpy(weights, h->w, sizeof(double) * (size_t)d);
+    if (iterations_run) *iterations_run = h->iter;
+  });
+}
+
+int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
+                         const double* weights, double intercept, double threshold, double* out,
+                         int mem) {
+  return guarded([&] {
+    if (!ctx || !weights) fail(EEGFX_EINVAL, "null argument");
+    check_mem(mem);
+    if (n < 0 || d < 1 || d > kLrMaxFeatures) fail(EEGFX_EINVAL, "n=%lld d=%d", (long long)n, d);
+    if (n == 0) return;
+    if (!X || !out) fail(EEGFX_EINVAL, "null X / out");
+    ctx->activate();
+    const double* dX = X;
+    double* dout = out;
+    if (mem == EEGFX_MEM_HOST) {
+      double* bx = (double*)ctx->lr_x.get(sizeof(double) * (size_t)(n * d));
+      HIP_CHECK(hipMemcpyAsync(bx, X, sizeof(double) * (size_t)(n * d), hipMemcpyHostToDevice,
+                               ctx->stream));
+      dX = bx;
+      dout = (double*)ctx->lr_y.get(sizeof(double) * (size_t)n);
+    }
+    const size_t sbytes = sizeof(LrState) + sizeof(double) * (size_t)d;
+    LrState* st = (LrState*)ctx->lr_state.get(sbytes);
+    HIP_CHECK(hipMemcpyAsync(st->w, weights, sizeof(double) * (size_t)d, hipMemcpyHostToDevice,
+                             ctx->stream));
+    const bool use_t = !std::isnan(threshold);  // LogisticRegressionModel.clearThreshold -> scores
+    HIP_CHECK(launch_lr_predict(ctx->stream, dX, n, d, st->w, intercept, threshold, use_t ? 1 : 0,
+                                dout));
+    if (mem == EEGFX_MEM_HOST)
+      HIP_CHECK(hipMemcpyAsync(out, dout, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
   });
 }
 

@@ -61,4 +61,21 @@ void dwt8_operator(double* M);
 void dwt8_operator_rows(double* rows);
 constexpr int kOperatorRowDoubles = 2 * 512;
 
+// logreg.hip: MLlib LogisticRegressionWithSGD (full batch) on device.  State block: iteration
+// count, flag (0 running, 1 converged / done, 2 invalid labels), then the d weights.
+struct LrState {
+  int32_t iter;
+  int32_t converged;
+  int32_t pad[2];
+  double w[];
+};
+constexpr int kLrMaxFeatures = 1024;
+int lr_grid(int64_t n);
+hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrState* state);
+hipError_t launch_lr_iteration(hipStream_t st, const double* X, const double* y, int64_t n, int d,
+                               LrState* state, double* partial, int G, double step_size,
+                               double reg, double tol, int max_iter);
+hipError_t launch_lr_predict(hipStream_t st, const double* X, int64_t n, int d, const double* w,
+                             double intercept, double threshold, int use_threshold, double* out);
+
 }  // namespace eegfx

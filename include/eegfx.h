@@ -185,6 +185,26 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
                                      const int64_t* pos, int64_t n_epochs, double* features,
                                      int64_t chunk_frames);
 
+/* ---- the downstream classifier ----------------------------------------
+ * LogisticRegressionClassifier.java:85-114 trains Spark MLlib 1.6.2 LogisticRegressionWithSGD on
+ * the feature rows: the default constructor (step 1.0, 100 iterations, regParam 0.01, fraction
+ * 1.0) or, with the config_* keys, the static train(...) with regParam 0.0.  This runs that
+ * full-batch gradient descent on the device: LogisticGradient, SquaredL2Updater with
+ * step/sqrt(i), GradientDescent's convergence test (||w_prev - w|| < tol * max(||w||, 1), MLlib's
+ * tol = 0.001), no intercept.  X is n x d row-major (the feature matrix as produced), y the 0/1
+ * labels; `weights` holds the initial weights (zeros in MLlib) on entry and the trained ones on
+ * return (host array).  mini_batch_fraction must be 1.0 (EEGFX_ENOTSUP otherwise: Spark's sampler
+ * depends on its partitioning); labels other than 0/1 give EEGFX_EINVAL ("Input validation
+ * failed").  eegfx_logreg_predict: LogisticRegressionModel.predict -- score = 1/(1+exp(-(w.x+b))),
+ * out = score > threshold ? 1 : 0, or the score itself when threshold is NaN (clearThreshold). */
+int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
+                           int32_t num_iterations, double step_size, double reg_param,
+                           double mini_batch_fraction, double convergence_tol, double* weights,
+                           int32_t* iterations_run, int mem);
+int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
+                         const double* weights, double intercept, double threshold, double* out,
+                         int mem);
+
 /* ---- multi-GPU ------------------------------------------------------------
  * Epochs shard by contiguous ranges of the selected-epoch list (eegfx_shard_range: balanced, the
  * first n % world ranks take one more); each rank runs the fused path on its range with no

@@ -1,0 +1,113 @@
+"""GPU logistic regression against the MLlib 1.6.2 restatement
+(oracle/mllib_logreg.py).  Spark's gradient sum order depends on its partitioning, so the bar is a
+tolerance: weights within 1e-9 relative (||w_gpu - w_oracle|| <= 1e-9 ||w_oracle||), the same
+iteration count, identical 0/1 predictions away from the 0.5 boundary.  Parity unpinned against
+the reference itself (no fixture holds trained weights)."""
+import numpy as np
+import pytest
+import torch
+
+import eeg_dataanalysispackage_amd as fx
+from eeg_dataanalysispackage_amd import classification as clf
+from eeg_dataanalysispackage_amd.pipeline import train_test_features
+from conftest import INFO_TRAIN
+from oracle import mllib_logreg as ref
+
+pytestmark = pytest.mark.gpu
+REL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = fx.Context(0, numerics="exact")
+    yield c
+    c.close()
+
+
+def rows(n, d, seed):
+    """Unit-norm rows (like the normalised features) with a planted separating direction."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, d))
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    w0 = rng.standard_normal(d)
+    y = (X @ w0 + 0.3 * rng.standard_normal(n) > 0).astype(np.float64)
+    return X, y
+
+
+def close(a, b):
+    return np.linalg.norm(a - b) <= REL * max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("n,d,reg", [(1, 48, 0.0), (37, 48, 0.0), (5000, 48, 0.01),
+                                     (20000, 48, 0.0), (3000, 512, 0.01), (257, 3, 0.0),
+                                     (100, 1000, 0.0)])
+def test_sgd_matches_mllib_restatement(ctx, n, d, reg):
+    X, y = rows(n, d, n + d)
+    w, it = clf.sgd_train(ctx, X, y, 100, 1.0, reg)
+    wr, itr = ref.sgd_train(X, y, 100, 1.0, reg)
+    assert it == itr
+    assert close(w, wr)
+
+
+def test_device_inputs_and_early_convergence(ctx):
+    X, y = rows(4000, 48, 7)
+    # a loose tolerance stops GradientDescent after a few iterations (never before the 2nd)
+    w, it = clf.sgd_train(ctx, torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), 100, 1.0,
+                          0.0, convergence_tol=0.3)
+    wr, itr = ref.sgd_train(X, y, 100, 1.0, 0.0, convergence_tol=0.3)
+    assert 2 <= it == itr < 100
+    assert close(w, wr)
+    w0, it0 = clf.sgd_train(ctx, X, y, 0)
+    assert it0 == 0 and not np.any(w0)
+
+
+def test_predict(ctx):
+    X, y = rows(3001, 48, 11)
+    w, _ = ref.sgd_train(X, y, 100, 1.0, 0.0)
+    score = ref.predict(X, w, threshold=None)
+    safe = np.abs(score - 0.5) > 1e-9
+    p = clf.predict(ctx, X, w)
+    assert np.array_equal(p[safe], ref.predict(X, w)[safe])
+    s = clf.predict(ctx, X, w, threshold=None)
+    assert np.max(np.abs(s - score)) <= 1e-12
+    pd = clf.predict(ctx, torch.from_numpy(X).cuda(), w)
+    torch.cuda.synchronize()
+    assert np.array_equal(pd.cpu().numpy(), p)
+
+
+def test_errors(ctx):
+    X, y = rows(50, 48, 3)
+    y[7] = 2.0
+    with pytest.raises(fx.EegfxError, match="validation"):
+        clf.sgd_train(ctx, X, y)
+    y[7] = 1.0
+    with pytest.raises(fx.EegfxError):
+        clf.sgd_train(ctx, X, y, mini_batch_fraction=0.5)  # Spark's partitioned sampler
+    with pytest.raises(fx.EegfxError):
+        clf.sgd_train(ctx, np.zeros((0, 48)), np.zeros(0))
+    with pytest.raises(fx.EegfxError):
+        clf.sgd_train(ctx, np.zeros((4, 2000)), np.zeros(4))
+
+
+def test_classifier_flow_on_info_txt(ctx):
+    """ClassifierTest.java:63-104 on the GPU: provider -> shuffle/split -> train -> test."""
+    odp = fx.OffLineDataProvider([INFO_TRAIN], context=ctx)
+    odp.loadData()
+    fe = fx.WaveletTransform(8, 512, 175, 16, context=ctx)
+    Xtr, ytr, Xte, yte = train_test_features(odp, fe)
+    c = clf.LogisticRegressionClassifier(context=ctx)
+    data, labels = odp.getData(), odp.getDataLabels()
+    from eeg_dataanalysispackage_amd.pipeline import reference_split
+    tr, te = reference_split(len(labels))
+    c.train(data[tr], [labels[i] for i in tr], fe)                 # default run(): regParam 0.01
+    wr, itr = ref.sgd_train(Xtr, ytr, 100, 1.0, 0.01)
+    assert c.iterations_run == itr and close(c.weights, wr)
+    stats = c.test(data[te], [labels[i] for i in te])
+    want = ref.reference_statistics(ref.predict(Xte, wr), yte)
+    assert stats.as_tuple() == want
+    assert stats.getNumberOfPatterns() == len(te)
+    c.setConfig({"config_num_iterations": "10", "config_step_size": "1.0",
+                 "config_mini_batch_fraction": "1.0"})
+    c.train(data[tr], [labels[i] for i in tr], fe)                 # static train(): regParam 0
+    wr, itr = ref.sgd_train(Xtr, ytr, 10, 1.0, 0.0)
+    assert c.iterations_run == itr and close(c.weights, wr)

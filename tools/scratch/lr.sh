@@ -1,0 +1,3 @@
+#!/bin/bash
+set -euo pipefail
+timeout -k 10 300 python -u -m pytest tests/test_gpu_logreg.py -m gpu -x -v --timeout 120 --timeout-method thread 2>&1 | tail -20
