@@ -73,6 +73,10 @@ def parse():
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather leg")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="rehearsal only: 'gloo' runs the N>1 control flow without RCCL")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (a one-GPU box)")
     return ap.parse_args()
 
 
@@ -105,10 +109,13 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     distributed = world > 1
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import eeg_dataanalysispackage_amd as fx
 
@@ -122,7 +129,7 @@ def main():
         args.epochs = 250_000  # 16 GB recording + 1 GB of 512-dim features per GPU
     n = args.epochs
     n_frames = FRAMES_PER_EPOCH * n + 2000
-    ctx = fx.Context(local, numerics=args.numerics)
+    ctx = fx.Context(dev.index, numerics=args.numerics)
     # A dedicated (non-null) torch stream shared with the context: the kernels run on it, so the
     # HIP events recorded on it bracket exactly the launches of the timed region.
     stream = torch.cuda.Stream(dev)
