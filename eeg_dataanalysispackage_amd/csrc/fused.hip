@@ -62,7 +62,6 @@ namespace dev {
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4_a16 __attribute__((ext_vector_type(4), aligned(16)));
 
-constexpr int kTile = 64;  // epochs per baseline workgroup (one per lane)
 constexpr int kSub = 8;    // epochs per window sub-tile (8 epochs x 8 segments = 64 lanes)
 
 constexpr int round_up_res(int v, int mod, int res) {  // smallest x >= v with x % mod == res
@@ -119,21 +118,21 @@ __device__ __forceinline__ bool straddles_end(int64_t A, int64_t nbytes, bool wa
   return want && A >= 0 && A < nbytes && A + 16 > nbytes;
 }
 
-template <int CT, int C>
-__global__ __launch_bounds__(64 * C) void baseline_kernel(
+template <int CT, int C, int TILE>
+__global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
     int64_t n, float* __restrict__ bout) {
   using G = Geometry<CT>;
-  constexpr int NT = 64 * C;
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kTile * G::BSTR];
-  __shared__ int64_t tB[kTile];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NT = (TILE * C + 63) / 64 * 64;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[TILE * G::BSTR];
+  __shared__ int64_t tB[TILE];
+  const int tid = threadIdx.x;
   const int64_t nbytes = n_frames * G::FB;
-  const int64_t t0 = (int64_t)blockIdx.x * kTile;
-  const int nt = (n - t0) < kTile ? (int)(n - t0) : kTile;
-  if (tid < kTile) tB[tid] = tid < nt ? (pos[t0 + tid] - kPre) * G::FB : 0;
+  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
+  if (tid < TILE) tB[tid] = tid < nt ? (pos[t0 + tid] - kPre) * G::FB : 0;
   __syncthreads();
-  constexpr int ITERS = (kTile * G::BASEQ + NT - 1) / NT;  // 13
+  constexpr int ITERS = (TILE * G::BASEQ + NT - 1) / NT;
   u32x4_a4 v[ITERS];
   int64_t A[ITERS];
   bool want[ITERS];
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(64 * C) void baseline_kernel(
   for (int k = 0; k < ITERS; ++k) {
     const int i = tid + k * NT;
     const int e = i / G::BASEQ, q = i - e * G::BASEQ;
-    want[k] = i < kTile * G::BASEQ && e < nt;
+    want[k] = i < TILE * G::BASEQ && e < nt;
     A[k] = want[k] ? (tB[e] & ~(int64_t)15) + 16 * q : 0;
     v[k] = load16_bulk(raw, nbytes, A[k], want[k] && !tiny);
   }
@@ -152,13 +151,14 @@ __global__ __launch_bounds__(64 * C) void baseline_kernel(
 #pragma unroll
   for (int k = 0; k < ITERS; ++k) {
     const int i = tid + k * NT;
-    if (i < kTile * G::BASEQ) {
+    if (i < TILE * G::BASEQ) {
       const int e = i / G::BASEQ, q = i - e * G::BASEQ;
       lds_store4(stage + e * G::BSTR + 4 * q, v[k]);
     }
   }
   __syncthreads();
-  const int c = w, e = lane;
+  if (tid >= TILE * C) return;
+  const int c = tid / TILE, e = tid - c * TILE;
   const float r = sel.res[c];
   const int16_t* src = (const int16_t*)((const uint8_t*)(stage + e * G::BSTR) + (tB[e] & 15)) +
                        sel.col[c];
@@ -167,7 +167,6 @@ __global__ __launch_bounds__(64 * C) void baseline_kernel(
   for (int i = 0; i < kPre; ++i) b = b + (float)src[i * CT] * r;
   if (e < nt) bout[(t0 + e) * C + c] = b / (float)kPre;
 }
-
 
 // Byte offset of sub-tile epoch e's window: B_e = (pos + 175) * FB; quads are fetched from
 // floor16(B_e) and the lanes fold (B_e & 15) into their read base.  e0 and e are wave-uniform,
@@ -956,9 +955,9 @@ hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_fram
                                  void* scratch) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
-  const dim3 bgrid((unsigned)((n + dev::kTile - 1) / dev::kTile));
-  hipLaunchKernelGGL((dev::baseline_kernel<3, 3>), bgrid, dim3(192), 0, st, (const uint8_t*)raw,
-                     n_frames, sel, pos, n, (float*)scratch);
+  // 64 epochs per workgroup; 16/32/128 measured the same or slower
+  hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), dim3((unsigned)((n + 63) / 64)), dim3(192),
+                     0, st, (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch);
   return hipGetLastError();
 }
 
