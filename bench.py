@@ -62,7 +62,7 @@ def parse():
                          "streamed to the device in chunks); logreg: the downstream classifier "
                          "(MLlib LogisticRegressionWithSGD, 100 full-batch iterations) on the 1M "
                          "48-dim feature rows of c3")
-    ap.add_argument("--chunk-frames", type=int, default=1 << 22, help="stream workload chunk")
+    ap.add_argument("--chunk-frames", type=int, default=1 << 23, help="stream workload chunk")
     ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
@@ -319,6 +319,28 @@ def bench_stream(args, rank, world, dev, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
     ok = bool(np.all(np.isfinite(out)) and np.max(np.abs(np.linalg.norm(out, axis=1) - 1)) < 1e-12)
+    # the host-link bound of a step: the same bytes moved by plain concurrent copies (the
+    # recording host -> device on one stream, the feature rows device -> host on another)
+    d_in = torch.empty(nf * 3, dtype=torch.int16, device=dev)
+    d_out = torch.empty((n, 48), dtype=torch.float64, device=dev)
+    h_out = torch.from_numpy(out)
+    s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    flat = host.view(-1)
+
+    def copies():
+        with torch.cuda.stream(s_in):
+            d_in.copy_(flat, non_blocking=True)
+        with torch.cuda.stream(s_out):
+            h_out.copy_(d_out, non_blocking=True)
+
+    copies()
+    torch.cuda.synchronize(dev)
+    c0 = time.perf_counter()
+    for _ in range(5):
+        copies()
+    torch.cuda.synchronize(dev)
+    copy_ms = (time.perf_counter() - c0) / 5 * 1e3
+    del d_in, d_out
     if rank == 0:
         h2d = nf * 6 * args.steps / el / 1e9
         print(json.dumps({
@@ -331,8 +353,12 @@ def bench_stream(args, rank, world, dev, dist):
                                    f"{args.chunk_frames}-frame chunks",
                        "epochs_per_gpu": n, "numerics": args.numerics, "unit_rows_check": ok},
             "host_link": {"bound": "pcie", "h2d_GBps": round(h2d, 2),
-                          "bytes_per_step": nf * 6,
-                          "note": "every frame crosses the host link once per step"},
+                          "bytes_per_step": nf * 6, "d2h_bytes_per_step": n * 48 * 8,
+                          "copy_only_ms": round(copy_ms, 3),
+                          "frac": round(copy_ms / (el / args.steps * 1e3), 4),
+                          "note": "every frame crosses the host link once per step and every "
+                                  "feature row once back; copy_only_ms = the same bytes moved by "
+                                  "two concurrent plain copies (the bound), frac = that / step"},
         }), flush=True)
     ctx.close()
 

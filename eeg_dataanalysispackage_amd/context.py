@@ -145,7 +145,7 @@ class Context:
         return out
 
     def process_recording_streamed(self, raw, n_channels_total: int, cols, res, pos,
-                                   chunk_frames: int = 1 << 22, out=None):
+                                   chunk_frames: int = 1 << 23, out=None):
         """configs[4]: the fused path over a host-resident recording streamed to the device in
         chunks (eegfx_process_recording_streamed); raw/pos/out are host (numpy) arrays."""
         cols_a, res_a = self._sel(cols, res)

@@ -107,6 +107,30 @@ struct eegfx_ctx {
   DevBuf lr_x, lr_y, lr_state, lr_part;  // logistic regression (eegfx_logreg_*)
   DevBuf mop;  // dwt-8 operator rows for EEGFX_MFMA (uploaded on first use)
   bool mop_ready = false;
+  // streamed path (eegfx_process_recording_streamed): upload / download streams and the chunk
+  // events, created on first use and kept for the context's lifetime
+  hipStream_t up = nullptr, down = nullptr;
+  static constexpr int kRing = 4;  // device chunk buffers in flight
+  hipEvent_t copied[kRing] = {}, done[kRing] = {};
+  void stream_resources() {
+    if (up) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+    for (int b = 0; b < kRing; ++b) {
+      HIP_CHECK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+    }
+  }
+  void release_stream_resources() {
+    for (int b = 0; b < kRing; ++b) {
+      if (copied[b]) (void)hipEventDestroy(copied[b]);
+      if (done[b]) (void)hipEventDestroy(done[b]);
+      copied[b] = done[b] = nullptr;
+    }
+    if (up) (void)hipStreamDestroy(up);
+    if (down) (void)hipStreamDestroy(down);
+    up = down = nullptr;
+  }
 
   const double* operator_rows() {
     if (!mop_ready) {
@@ -543,6 +567,11 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     ctx->scratch.release();
     ctx->fused.release();
     ctx->mop.release();
+    ctx->lr_x.release();
+    ctx->lr_y.release();
+    ctx->lr_state.release();
+    ctx->lr_part.release();
+    ctx->release_stream_resources();
     ctx->destroy_events();
     (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -656,10 +685,12 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
 // chunks of `chunk_frames` frames.  Epochs are taken in position order; a chunk starts at the
 // first unprocessed epoch's baseline frame (pos - 100) and holds every following epoch whose
 // frames [pos-100, pos+687) fit (or reach past the recording end, which the kernels zero-pad), so
-// consecutive chunks overlap by at most one epoch span (787 frames) -- the halo.  Two device
-// chunk buffers and a copy stream overlap the H2D of chunk k+1 with the kernels of chunk k; a
-// pageable source is first copied into one of two pinned staging buffers on the calling thread
-// (that copy overlaps the device work of the previous chunk), a pinned source (hipHostMalloc /
+// consecutive chunks overlap by at most one epoch span (787 frames) -- the halo.  A ring of four
+// device chunk buffers and an upload stream let the H2D run up to three chunks ahead of the
+// kernels, and each chunk's rows leave on a download stream as soon as its kernels finish (the
+// host link runs both directions at once; with two buffers the event hops between streams
+// stalled the uploads).  A pageable source is first copied into one of two pinned staging
+// buffers by host threads (that copy overlaps the device work), a pinned source (hipHostMalloc /
 // registered) is copied directly.
 int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fmt,
                                      int64_t n_frames, int32_t ct, const int32_t* cols,
@@ -703,48 +734,51 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
     // (rounded to 256 B so the second buffer is as aligned as the first: the kernels read
     // 16-byte quads relative to `raw`)
     const size_t cbytes = ((size_t)(chunk_frames * FB) + 128 + 255) & ~(size_t)255;
-    uint8_t* dbuf = (uint8_t*)ctx->raw.get(2 * cbytes);
+    constexpr int R = eegfx_ctx::kRing;
+    uint8_t* dbuf = (uint8_t*)ctx->raw.get(R * cbytes);
     hipPointerAttribute_t attr;
     const bool pinned = hipPointerGetAttributes(&attr, raw) == hipSuccess &&
                         attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();  // a pageable pointer can leave an error behind
     void* pin[2] = {nullptr, nullptr};
-    hipStream_t cs = nullptr, os = nullptr;  // upload (H2D) and download (D2H) streams
-    hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    ctx->stream_resources();
+    hipStream_t cs = ctx->up, os = ctx->down;  // upload (H2D) and download (D2H) streams
+    hipEvent_t* copied = ctx->copied;
+    hipEvent_t* done = ctx->done;
     auto cleanup = [&] {
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < 2; ++b)
         if (pin[b]) (void)hipHostFree(pin[b]);
-        if (copied[b]) (void)hipEventDestroy(copied[b]);
-        if (done[b]) (void)hipEventDestroy(done[b]);
-      }
-      if (cs) (void)hipStreamDestroy(cs);
-      if (os) (void)hipStreamDestroy(os);
+    };
+    // Chunk sizes ramp up (c/4, c/2, then c) and down (about half of what remains, not below
+    // c/4) so that the first upload and the last download -- the parts of a call that nothing
+    // overlaps -- stay short.
+    const int64_t last = spos[n - 1] - EEGFX_PRESTIMULUS + kSpan;
+    auto chunk_at = [&](int64_t k, int64_t lo) {
+      int64_t c = k < 2 ? chunk_frames >> (2 - k) : chunk_frames;
+      const int64_t rest = last - lo;
+      if (rest < 2 * chunk_frames) c = std::min(c, (rest + 1) / 2);
+      return std::min(chunk_frames, std::max(c, std::max(chunk_frames / 4, 2 * kSpan)));
     };
     try {
-      HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-      HIP_CHECK(hipStreamCreateWithFlags(&os, hipStreamNonBlocking));
-      for (int b = 0; b < 2; ++b) {
-        HIP_CHECK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+      for (int b = 0; b < 2; ++b)
         if (!pinned) HIP_CHECK(hipHostMalloc(&pin[b], cbytes, hipHostMallocDefault));
-      }
       HIP_CHECK(hipStreamSynchronize(ctx->stream));  // d_pos uploaded; buffers idle
       int64_t i = 0, k = 0;
       while (i < n) {
-        const int b = (int)(k & 1);
+        const int b = (int)(k % R);
         const int64_t lo = spos[i] - EEGFX_PRESTIMULUS;
-        const int64_t hi = std::min(lo + chunk_frames, n_frames);
+        const int64_t hi = std::min(lo + chunk_at(k, lo), n_frames);
         int64_t j = i;
         while (j < n && (spos[j] - EEGFX_PRESTIMULUS + kSpan <= hi || hi == n_frames)) ++j;
         const int64_t Lb = (lo * FB) & ~(int64_t)15, Hb = hi * FB;
         const size_t bytes = Hb > Lb ? (size_t)(Hb - Lb) : 0;
         uint8_t* dst = dbuf + (size_t)b * cbytes + 64;
-        if (k >= 2) HIP_CHECK(hipStreamWaitEvent(cs, done[b], 0));  // kernels of chunk k-2 done
+        if (k >= R) HIP_CHECK(hipStreamWaitEvent(cs, done[b], 0));  // kernels of chunk k-R done
         const uint8_t* src = (const uint8_t*)raw + Lb;
-        if (!pinned) {
-          if (k >= 2) HIP_CHECK(hipEventSynchronize(copied[b]));  // staging b drained
-          if (bytes) parallel_memcpy(pin[b], src, bytes);
-          src = (const uint8_t*)pin[b];
+        if (!pinned) {  // two pinned staging buffers: staging k&1 is free once chunk k-2 uploaded
+          if (k >= 2) HIP_CHECK(hipEventSynchronize(copied[(k - 2) % R]));
+          if (bytes) parallel_memcpy(pin[k & 1], src, bytes);
+          src = (const uint8_t*)pin[k & 1];
         }
         if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs));
         HIP_CHECK(hipEventRecord(copied[b], cs));
