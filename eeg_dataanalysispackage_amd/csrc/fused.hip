@@ -193,6 +193,23 @@ __device__ __forceinline__ void decode_pairs(const int16_t (&xr)[kIn], float r, 
   }
 }
 
+// decode_pairs reading the samples straight from the staged window: own[k*CT] for k < 64, then
+// the 8 halo samples nxt[k*CT] of the next segment.
+template <int CT, int N = kIn>
+__device__ __forceinline__ void decode_lds(const int16_t* own, const int16_t* nxt, float r, float b,
+                                           double (&x)[kIn]) {
+  const f32x2 rr = {r, r}, bb = {b, b};
+#pragma unroll
+  for (int k = 0; k < N; k += 2) {
+    const int16_t v0 = k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT];
+    const int16_t v1 = k + 1 < kSegLen ? own[(k + 1) * CT] : nxt[(k + 1 - kSegLen) * CT];
+    const f32x2 v = {(float)v0, (float)v1};
+    const f32x2 y = v * rr - bb;
+    x[k] = (double)y.x;
+    x[k + 1] = (double)y.y;
+  }
+}
+
 // SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
 // sub-tile, executed by one wave: lane e < ne folds Math.pow(f, 2) over row e in index order
 // (the 8 dependent chains run side by side), then the 64 lanes divide and store the rows
@@ -402,15 +419,20 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + tdelta[kk & 1][el] + 2 * col;
     const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
     const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
+    // With one sub-tile per workgroup nothing refills the window, so the samples are decoded
+    // straight from LDS (no int16 staging array: 72 fewer live VGPRs, no spill); with K > 1
+    // they are copied to registers first and barrier A frees the window for the next DMA.
     int16_t xr[kIn];
+    if constexpr (K > 1) {
 #pragma unroll
-    for (int k = 0; k < kSegLen; ++k) xr[k] = own[k * CT];
-    if constexpr (!EEGFX_HALO0_SHFL) {
+      for (int k = 0; k < kSegLen; ++k) xr[k] = own[k * CT];
+      if constexpr (!EEGFX_HALO0_SHFL) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nxt[k * CT];
+        for (int k = 0; k < 8; ++k) xr[kSegLen + k] = nxt[k * CT];
+      }
     }
     const float b = bcur;
-    __syncthreads();  // (A) every lane holds its samples: the window is free
+    if constexpr (K > 1) __syncthreads();  // (A) every lane holds its samples: the window is free
     // 2. the next sub-tile streams into the window while the filter bank runs
     const int64_t e1 = e0 + kSub;
     const bool more = kk + 1 < K && e1 < n;
@@ -425,6 +447,9 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     if constexpr (EEGFX_FUSED_ABLATION & 2) {
 #pragma unroll
       for (int k = 0; k < kIn; ++k) x[k] = (double)b + k;
+    } else if constexpr (K == 1) {
+      decode_lds<CT, EEGFX_HALO0_SHFL ? kSegLen : kIn>(own, nxt, r, b, x);
+      if constexpr (EEGFX_HALO0_SHFL) halo_shuffle<kSegLen>(x, lane & ~7, s);
     } else if constexpr (EEGFX_HALO0_SHFL) {
       decode_pairs<kSegLen>(xr, r, b, x);
       halo_shuffle<kSegLen>(x, lane & ~7, s);
@@ -441,8 +466,13 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       dwt8_cascade<FAST, SHFL>(x, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
     }
     double* fb = feat[kk & 1];
-    fb[el * F + w * 16 + s] = a6;
-    fb[el * F + w * 16 + 8 + s] = d6;
+    // the row slot is recomputed here from an opaque copy of the lane id, so its address is not
+    // kept live across the filter bank (it was the one spilled VGPR)
+    int l2 = lane;
+    asm volatile("" : "+v"(l2));
+    const int slot = (l2 >> 3) * F + w * 16 + (l2 & 7);
+    fb[slot] = a6;
+    fb[slot + 8] = d6;
     if (need_fix) dma_fixup<CT, C>(raw, nbytes, pos, n, e1, win, w, lane, rows);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (B) features(kk) and window(kk+1) complete
