@@ -55,6 +55,11 @@
 #ifndef EEGFX_HALO0_SHFL
 #define EEGFX_HALO0_SHFL 0
 #endif
+// Decode of the K == 1 kernel: 0 = two samples per packed fp32 op, 1 = one sample per op (72
+// more VALU ops per wave, but 96 instead of 116 VGPRs: 5 waves/SIMD, measured 2 % faster).
+#ifndef EEGFX_DECODE_SCALAR
+#define EEGFX_DECODE_SCALAR 1
+#endif
 
 namespace eegfx {
 namespace dev {
@@ -198,6 +203,14 @@ __device__ __forceinline__ void decode_pairs(const int16_t (&xr)[kIn], float r, 
 template <int CT, int N = kIn>
 __device__ __forceinline__ void decode_lds(const int16_t* own, const int16_t* nxt, float r, float b,
                                            double (&x)[kIn]) {
+#if EEGFX_DECODE_SCALAR
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int16_t v0 = k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT];
+    x[k] = (double)((float)v0 * r - b);
+  }
+  return;
+#endif
   const f32x2 rr = {r, r}, bb = {b, b};
 #pragma unroll
   for (int k = 0; k < N; k += 2) {
@@ -391,7 +404,9 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   using G = Geometry<CT>;
   constexpr int F = C * 16;
   __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
-  __shared__ __attribute__((aligned(16))) double feat[2][kSub * F];
+  // K > 1: double-buffered feature rows; K == 1: the rows reuse the start of the window buffer
+  // once every wave has decoded its samples (26 KB of LDS per workgroup instead of 32)
+  __shared__ __attribute__((aligned(16))) double feat[K > 1 ? 2 : 1][K > 1 ? kSub * F : 2];
   __shared__ int tdelta[2][kSub];
   __shared__ double norm[kSub];
   __shared__ __attribute__((aligned(16))) double xch[SHFL ? 2 : C * 64 * kSlot];
@@ -465,7 +480,8 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     } else {
       dwt8_cascade<FAST, SHFL>(x, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
     }
-    double* fb = feat[kk & 1];
+    double* fb = K > 1 ? feat[kk & 1] : (double*)win;
+    if constexpr (K == 1) __syncthreads();  // every wave has read its samples: rows may overwrite
     // the row slot is recomputed here from an opaque copy of the lane id, so its address is not
     // kept live across the filter bank (it was the one spilled VGPR)
     int l2 = lane;
@@ -925,7 +941,7 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
                        (const uint8_t*)raw, n_frames, sel, pos, base, n, out);                    \
     launched = true;                                                                              \
   }
-  EEGFX_D(4, 1, true) EEGFX_D(3, 1, true) EEGFX_D(2, 2, true) EEGFX_D(3, 2, true)
+  EEGFX_D(4, 1, true) EEGFX_D(5, 1, true) EEGFX_D(3, 1, true) EEGFX_D(2, 2, true) EEGFX_D(3, 2, true)
   EEGFX_D(4, 2, true) EEGFX_D(4, 4, true) EEGFX_D(4, 8, true) EEGFX_D(3, 4, true)
   EEGFX_D(3, 1, false) EEGFX_D(3, 2, false)
 #undef EEGFX_D
