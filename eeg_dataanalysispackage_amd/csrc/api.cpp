@@ -245,7 +245,8 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   }
   double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
   ctx->tic();
-  HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep));
+  HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep,
+                              ctx->fused.get(fused_scratch_bytes(n, C))));
   HIP_CHECK(launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
                                         EEGFX_DWT8_FEATURE_SIZE, fast, out));
   ctx->toc(0);
@@ -419,7 +420,8 @@ struct eegfx_odp {
     HIP_CHECK(hipMemcpyAsync(d_pos, pos.data(), sizeof(int64_t) * (size_t)k,
                              hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, h.info.binary_format, n_frames, ct, sel, 3,
-                                d_pos, k, (double*)((char*)d_epochs.p + per * (size_t)n_epochs)));
+                                d_pos, k, (double*)((char*)d_epochs.p + per * (size_t)n_epochs),
+                                ctx->fused.get(fused_scratch_bytes(k, 3))));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     n_epochs += k;
     positions.insert(positions.end(), pos.begin(), pos.end());
@@ -620,7 +622,8 @@ int eegfx_cut_epochs_f64(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n
     const int64_t* d_pos = (const int64_t*)stage_in(ctx, ctx->pos, pos, sizeof(int64_t) * n, mem);
     double* d_out = mem == EEGFX_MEM_DEVICE ? epochs_out : (double*)ctx->out.get(out_bytes);
     ctx->tic();
-    HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out));
+    HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out,
+                                ctx->fused.get(fused_scratch_bytes(n, C))));
     ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(epochs_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));

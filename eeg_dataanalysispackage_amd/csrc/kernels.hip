@@ -54,6 +54,30 @@ __global__ __launch_bounds__(256) void cut_epochs_kernel(const T* __restrict__ r
   }
 }
 
+// a5..a7 write pass of the materialised epochs (getData()): the per-(epoch, channel) baselines
+// come from the LDS-staged baseline kernels; each lane writes two consecutive samples of one
+// channel row as one 16-byte store (750 is even, so a pair never straddles two rows).
+template <typename T>
+__global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ raw, int64_t n_frames,
+                                                        int ct, ChanSel sel, int C,
+                                                        const int64_t* __restrict__ pos,
+                                                        const float* __restrict__ base,
+                                                        double* __restrict__ out) {
+  const int64_t e = blockIdx.x;
+  const int64_t p = pos[e];
+  double* o = out + e * C * kPost;
+  for (int idx = 2 * (int)threadIdx.x; idx < C * kPost; idx += 2 * (int)blockDim.x) {
+    const int c = idx / kPost;
+    const int64_t f = p + (idx - c * kPost);
+    const int col = sel.col[c];
+    const float r = sel.res[c], b = base[e * C + c];
+    // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
+    const float v0 = f < n_frames ? (float)raw[f * ct + col] * r : 0.0f;
+    const float v1 = f + 1 < n_frames ? (float)raw[(f + 1) * ct + col] * r : 0.0f;
+    *(double2*)(o + idx) = make_double2((double)(v0 - b), (double)(v1 - b));
+  }
+}
+
 // a11..a13 from materialised epochs.  A workgroup owns 8 epochs; wave w walks the channels
 // w, w+NW, ...; within a wave lane = 8*epoch + segment (dwt8.h).  Features are collected in LDS,
 // normalised per epoch with the reference's sequential sum of squares, and written coalesced.
@@ -142,9 +166,26 @@ __global__ __launch_bounds__(256) void synth_kernel(int16_t* __restrict__ dst, i
 // ---- launchers ---------------------------------------------------------------------------------
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                             double* out) {
+                             double* out, void* scratch) {
   if (n == 0) return hipSuccess;
   dim3 grid((unsigned)n), block(256);
+  // baselines by the staged kernels when a layout fits them, then the coalesced write pass
+  hipError_t be = hipErrorNotSupported;
+  const bool aligned = ((uintptr_t)out & 15) == 0;  // the write pass stores 16-byte pairs
+  if (!aligned) scratch = nullptr;
+  if (scratch && fmt == 0 && ct == 3 && C == 3)
+    be = launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch);
+  else if (scratch && baseline_any_supported(fmt, ct, C))
+    be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch);
+  if (be == hipSuccess) {
+    if (fmt == 0)
+      hipLaunchKernelGGL(dev::cut_write_kernel<int16_t>, grid, block, 0, st, (const int16_t*)raw,
+                         n_frames, ct, sel, C, pos, (const float*)scratch, out);
+    else
+      hipLaunchKernelGGL(dev::cut_write_kernel<float>, grid, block, 0, st, (const float*)raw,
+                         n_frames, ct, sel, C, pos, (const float*)scratch, out);
+    return hipGetLastError();
+  }
   if (fmt == 0)
     hipLaunchKernelGGL(dev::cut_epochs_kernel<int16_t>, grid, block, 0, st,
                        (const int16_t*)raw, n_frames, ct, sel, C, pos, out);

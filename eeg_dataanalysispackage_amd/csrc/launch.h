@@ -16,8 +16,10 @@ struct ChanSel {
   float res[kMaxChannels];
 };
 
+// scratch: fused_scratch_bytes(n, C) bytes for the baselines (nullptr: single-kernel fallback)
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
-                             const ChanSel& sel, int C, const int64_t* pos, int64_t n, double* out);
+                             const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                             double* out, void* scratch);
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
                                        int nfeat, bool fast, double* out);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
@@ -42,6 +44,7 @@ int64_t fused_window_bytes_per_epoch(int ct, int C);
 // contract as the 3-channel kernels.  wide_supported: int16/float32, C <= 64, one epoch's staged
 // window + features within 64 KB of LDS (int16: about 60 channels in the file).
 bool wide_supported(int fmt, int ct, int C);
+bool baseline_any_supported(int fmt, int ct, int C);
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                                void* scratch);

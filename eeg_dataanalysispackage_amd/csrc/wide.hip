@@ -259,14 +259,28 @@ bool wide_supported(int fmt, int ct, int C) {
          wide_lds_per_epoch(fmt, ct, C) <= 64 * 1024;
 }
 
-hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
-                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch) {
-  if (n == 0) return hipSuccess;
+static int baseline_any_tile(int fmt, int ct, int C, int* bstq) {
   const int FB = ct * (fmt == 0 ? 2 : 4);
   const int BSTQ = (dev::kPre * FB + 15) / 16 + 2;  // staged quads + 1 quad of bank skew
   int EB = 256 / C;  // lanes = (epoch, channel) pairs (<= 256 epochs: the sB table)
   while (EB > 1 && (size_t)EB * BSTQ * 16 > 56 * 1024) --EB;
+  if (bstq) *bstq = BSTQ;
+  return EB;
+}
+
+bool baseline_any_supported(int fmt, int ct, int C) {
+  if (!(fmt == 0 || fmt == 1) || C < 1 || C > 256 || ct < 1) return false;
+  int bstq = 0;
+  const int EB = baseline_any_tile(fmt, ct, C, &bstq);
+  return (size_t)EB * bstq * 16 <= 64 * 1024;
+}
+
+hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                               void* scratch) {
+  if (n == 0) return hipSuccess;
+  int BSTQ = 0;
+  const int EB = baseline_any_tile(fmt, ct, C, &BSTQ);
   const size_t lds = (size_t)EB * BSTQ * 16;
   const dim3 grid((unsigned)((n + EB - 1) / EB));
   if (fmt == 0)

@@ -126,6 +126,29 @@ def test_cut_epochs_exact(ctx):
               oracle.decode_epochs(raw, [2, 0, 1], [0.1, 0.25, 0.5], pos))
 
 
+def test_cut_epochs_device_paths(ctx):
+    """Device-resident cut: the two-pass kernels (staged baselines + 16-byte row writes) and the
+    single-kernel fallback taken for an output that is only 8-byte aligned."""
+    import torch
+    rng = np.random.default_rng(13)
+    raw = synth_raw(rng, 30000, 3)
+    pos = np.concatenate([[100], rng.integers(100, 30100, size=60), [30100]])
+    want = oracle.decode_epochs(raw, [0, 1, 2], [0.1] * 3, pos)
+    draw, dpos = torch.from_numpy(raw).cuda(), torch.from_numpy(pos).cuda()
+    got = ctx.cut_epochs(draw, 3, [0, 1, 2], [0.1] * 3, dpos)
+    ctx.synchronize()
+    assert eq(got.cpu().numpy(), want)
+    flat = torch.empty(len(pos) * 3 * 750 + 1, dtype=torch.float64, device="cuda")
+    odd = flat[1:].view(len(pos), 3, 750)          # 8-byte aligned only
+    ctx.cut_epochs(draw, 3, [0, 1, 2], [0.1] * 3, dpos, out=odd)
+    ctx.synchronize()
+    assert eq(odd.cpu().numpy(), want)
+    raw5 = synth_raw(rng, 20000, 5)                # generic layout: baseline_any + write pass
+    pos5 = rng.integers(100, 20100, size=40)
+    assert eq(ctx.cut_epochs(raw5, 5, [4, 1], [0.1, 0.3], pos5),
+              oracle.decode_epochs(raw5, [4, 1], [0.1, 0.3], pos5))
+
+
 def test_saturated_and_odd_positions(ctx):
     rng = np.random.default_rng(5)
     raw = synth_raw(rng, 20000, 3)
