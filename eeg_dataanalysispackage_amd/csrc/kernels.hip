@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
 template <bool FAST>
 __global__ __launch_bounds__(256) void features_from_epochs_kernel(const double* __restrict__ ep,
                                                                    int64_t n, int C, int skip,
-                                                                   int nfeat,
+                                                                   int nfeat, int row_stride,
                                                                    double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nw = blockDim.x / 64;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void features_from_epochs_kernel(const double*
   const bool valid = e < n;
   for (int c = w; c < C; c += nw) {
     double x[kIn];
-    const double* src = ep + (valid ? (e * C + c) * kPost + skip : 0);
+    const double* src = ep + (valid ? (e * C + c) * row_stride + skip : 0);
 #pragma unroll
     for (int k = 0; k < kIn; ++k) x[k] = valid ? src[(kSegLen * s + k) & (kWin - 1)] : 0.0;
     double a6, d6;
@@ -196,17 +196,17 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
 }
 
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
-                                       int nfeat, bool fast, double* out) {
+                                       int nfeat, bool fast, double* out, int row_stride) {
   if (n == 0) return hipSuccess;
   const int nw = C < 4 ? C : 4;
   const size_t smem = sizeof(double) * ((size_t)nw * 64 * dev::kSlot + 8 * (size_t)C * nfeat + 8);
   dim3 grid((unsigned)((n + 7) / 8)), block(64 * nw);
   if (fast)
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, out);
+                       skip, nfeat, row_stride, out);
   else
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<false>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, out);
+                       skip, nfeat, row_stride, out);
   return hipGetLastError();
 }
 

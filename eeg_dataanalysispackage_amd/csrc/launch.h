@@ -20,8 +20,10 @@ struct ChanSel {
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                              double* out, void* scratch);
+// row_stride: doubles between consecutive (epoch, channel) rows of `ep` (750 for materialised
+// epochs, 512 for the window-only rows the host path stages)
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
-                                       int nfeat, bool fast, double* out);
+                                       int nfeat, bool fast, double* out, int row_stride = 750);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
 // Fused raw -> features (fused.hip): baseline_kernel then window_kernel.  `scratch` holds

@@ -126,6 +126,29 @@ def test_cut_epochs_exact(ctx):
               oracle.decode_epochs(raw, [2, 0, 1], [0.1, 0.25, 0.5], pos))
 
 
+def test_extract_features_host_chunks(ctx):
+    """Host epochs (the IFeatureExtraction drop-in) go through window-only pinned staging in
+    8,192-epoch chunks: equal to the device-resident path and to the oracle."""
+    import torch
+    rng = np.random.default_rng(17)
+    n = 20001
+    raw = synth_raw(rng, 1000 * n + 2000, 3)
+    pos = np.arange(1000, 1000 * (n + 1), 1000)
+    dep = ctx.cut_epochs(torch.from_numpy(raw).cuda(), 3, [0, 1, 2], [0.1] * 3,
+                         torch.from_numpy(pos).cuda())
+    ctx.synchronize()
+    host = dep.cpu().numpy()
+    got = ctx.extract_features(host)
+    dev = ctx.extract_features(dep)
+    ctx.synchronize()
+    assert eq(got, dev.cpu().numpy())
+    sel = np.r_[0:50, 8180:8200, n - 30:n]
+    assert eq(got[sel], oracle.extract_features(host[sel]))
+    for nf, sk in ((5, 175), (16, 238)):
+        assert eq(ctx.extract_features(host[:9000], feature_size=nf, skip=sk),
+                  oracle.extract_features(host[:9000], nfeat=nf, skip=sk))
+
+
 def test_cut_epochs_device_paths(ctx):
     """Device-resident cut: the two-pass kernels (staged baselines + 16-byte row writes) and the
     single-kernel fallback taken for an output that is only 8-byte aligned."""
