@@ -54,3 +54,14 @@ def test_status_mapping_without_gpu():
     rc = fx.lib().eegfx_read_header(b"/nonexistent.vhdr", ctypes.byref(info), None, 0)
     assert rc == _lib.EEGFX_EIO
     assert b"cannot open" in fx.lib().eegfx_last_error()
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: with the shared object gone, every entry point raises."""
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libeegfx.so"))
+    import pytest
+    with pytest.raises(ImportError, match="missing"):
+        _lib.lib()
+    with pytest.raises(ImportError):
+        fx.Context(0)
