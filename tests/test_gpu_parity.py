@@ -311,13 +311,16 @@ def test_wide_fma_within_tolerance(ctx_fma, ct, cols):
 
 
 # ---- configs[4]: long recordings streamed from host memory in chunks -------------------------
-@pytest.mark.parametrize("chunk", [787, 1000, 4099, 1 << 20])
-def test_streamed_equals_resident(ctx, chunk):
+@pytest.mark.parametrize("chunk,ordered", [(787, False), (1000, False), (4099, False),
+                                           (1 << 20, False), (1600, True), (8192, True)])
+def test_streamed_equals_resident(ctx, chunk, ordered):
     rng = np.random.default_rng(chunk)
     nf = 60000
     raw = synth_raw(rng, nf, 3)
     pos = rng.integers(100, nf + 100, size=400)  # unsorted, overlapping, tails past the end
     pos[:3] = [100, nf + 100, nf - 50]
+    if ordered:  # the in-order fast path (rows leave per chunk) with ramped chunk sizes
+        pos = np.sort(pos)
     got = ctx.process_recording_streamed(raw, 3, [0, 1, 2], [0.1] * 3, pos, chunk_frames=chunk)
     assert eq(got, ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, pos))
     assert eq(got, oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos))
