@@ -89,6 +89,19 @@ __device__ __forceinline__ const uint8_t* safe_quad(const uint8_t* raw, int64_t 
   return nbytes >= 16 ? raw + ((nbytes & ~(int64_t)15) - 16) : raw;
 }
 
+// XCD-aware tile order (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"): blocks are dealt
+// round-robin over the 8 XCDs, so block b runs on the XCD of b % 8.  Renumbering the blocks so that
+// each XCD walks one contiguous range of tiles keeps tiles that share input bytes (overlapping
+// windows of dense markers) in the same L2.  Bijective for any grid size; a speed choice only.
+#ifndef EEGFX_XCD_REMAP
+#define EEGFX_XCD_REMAP 1
+#endif
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
+  if (!EEGFX_XCD_REMAP) return b;
+  const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // Orders LDS traffic of the lanes of one wave (DS ops of a wave execute in order; the fences
 // keep the compiler from moving them across this point).
 __device__ __forceinline__ void wave_sync() {

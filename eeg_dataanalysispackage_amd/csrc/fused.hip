@@ -416,7 +416,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   const int64_t nbytes = n_frames * G::FB;
   const int col = sel.col[w];
   const float r = sel.res[w];
-  const int64_t first = (int64_t)blockIdx.x * K * kSub;
+  const int64_t first = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * K * kSub;
 
   if (w == 0 && lane < kSub)
     tdelta[0][lane] = first + lane < n ? (int)(window_byte<CT>(pos, first + lane) & 15) : 0;

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   double* feat = (double*)(smem + (size_t)EPW * EQ * 16);
   double* norm = feat + EPW * F;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t e0 = (int64_t)blockIdx.x * EPW;
+  const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * EPW;
   const int ne = (n - e0) < EPW ? (int)(n - e0) : EPW;
   const int64_t nbytes = n_frames * FB;
 

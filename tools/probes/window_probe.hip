@@ -30,7 +30,9 @@ int main() {
   if (getenv("PROBE_RANDOM")) fill_random<<<4096, 256>>>((uint32_t*)raw, nf * 6 / 4);
   else (void)hipMemset(raw, 3, nf * 6);
   std::vector<int64_t> hp(n);
-  for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + 1000 * i;
+  const char* sp = getenv("PROBE_SPACING");  // frames between markers (1000: the bench)
+  const int64_t spacing = sp ? atoi(sp) : 1000;
+  for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + spacing * i;
   (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
   eegfx::ChanSel sel{};
   for (int c = 0; c < 3; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
