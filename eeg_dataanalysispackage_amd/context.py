@@ -144,6 +144,31 @@ class Context:
                                             ptr(pos), n, ptr(out), mem))
         return out
 
+    def plan_markers(self, positions, stimulus_index, n_frames: int, guessed: int,
+                     balance: int = 0):
+        """Marker planning (OffLineDataProvider.java:200-265) on the device as a parallel scan
+        (eegfx_plan_markers_device): returns (positions, labels, balance) like
+        brainvision.plan_markers.  positions / stimulus_index: host or device arrays."""
+        from ctypes import byref
+        if _is_device(positions):
+            import torch
+            n = int(positions.numel())
+            pos_out = torch.empty(max(1, n), dtype=torch.int64, device=positions.device)
+            lab_out = torch.empty(max(1, n), dtype=torch.float64, device=positions.device)
+        else:
+            positions = np.ascontiguousarray(positions, dtype=np.int64)
+            stimulus_index = np.ascontiguousarray(stimulus_index, dtype=np.int32)
+            n = positions.size
+            pos_out = np.empty(max(1, n), dtype=np.int64)
+            lab_out = np.empty(max(1, n), dtype=np.float64)
+        bal = c_int64(balance)
+        k = c_int64()
+        check(lib().eegfx_plan_markers_device(self.handle, ptr(positions), ptr(stimulus_index), n,
+                                              int(n_frames), int(guessed), byref(bal),
+                                              ptr(pos_out), ptr(lab_out), byref(k),
+                                              _mem(positions, stimulus_index, pos_out)))
+        return pos_out[:k.value], lab_out[:k.value], bal.value
+
     def process_recording_streamed(self, raw, n_channels_total: int, cols, res, pos,
                                    chunk_frames: int = 1 << 23, out=None):
         """configs[4]: the fused path over a host-resident recording streamed to the device in

@@ -938,6 +938,53 @@ int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
   });
 }
 
+int eegfx_plan_markers_device(eegfx_ctx* ctx, const int64_t* positions,
+                              const int32_t* stimulus_index, int64_t n_markers, int64_t n_frames,
+                              int32_t guessed, int64_t* balance, int64_t* pos_out,
+                              double* label_out, int64_t* n_selected, int mem) {
+  return guarded([&] {
+    if (!ctx || !balance || !n_selected) fail(EEGFX_EINVAL, "null argument");
+    check_mem(mem);
+    if (n_markers < 0) fail(EEGFX_EINVAL, "negative marker count");
+    if (*balance < -1 || *balance > 1)
+      fail(EEGFX_EINVAL, "balance %lld outside {-1, 0, 1}", (long long)*balance);
+    *n_selected = 0;
+    if (n_markers == 0) return;
+    if (!positions || !stimulus_index) fail(EEGFX_EINVAL, "null markers");
+    ctx->activate();
+    const int64_t n = n_markers;
+    const int64_t* d_pos = (const int64_t*)stage_in(ctx, ctx->pos, positions, sizeof(int64_t) * n,
+                                                    mem);
+    const int32_t* d_stim = (const int32_t*)stage_in(ctx, ctx->lr_y, stimulus_index,
+                                                     sizeof(int32_t) * n, mem);
+    int64_t* d_pos_out = pos_out;
+    double* d_label = label_out;
+    if (mem == EEGFX_MEM_HOST) {
+      uint8_t* o = (uint8_t*)ctx->out.get((sizeof(int64_t) + sizeof(double)) * (size_t)n);
+      d_pos_out = pos_out ? (int64_t*)o : nullptr;
+      d_label = label_out ? (double*)(o + sizeof(int64_t) * (size_t)n) : nullptr;
+    }
+    void* scratch = ctx->scratch.get(plan_scratch_bytes(n));
+    PlanResult r;
+    HIP_CHECK(launch_plan_markers(ctx->stream, d_pos, d_stim, n, n_frames, guessed,
+                                  (int)*balance, scratch, d_pos_out, d_label, &r));
+    if (mem == EEGFX_MEM_HOST && r.selected > 0) {
+      if (pos_out)
+        HIP_CHECK(hipMemcpyAsync(pos_out, d_pos_out, sizeof(int64_t) * (size_t)r.selected,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+      if (label_out)
+        HIP_CHECK(hipMemcpyAsync(label_out, d_label, sizeof(double) * (size_t)r.selected,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    *balance = r.balance;
+    *n_selected = r.selected;
+    if (r.first_unparsable >= 0)  // Integer.parseInt's NumberFormatException ends the reference loop
+      fail(EEGFX_EFORMAT, "marker %lld: unparsable stimulus description",
+           (long long)r.first_unparsable);
+  });
+}
+
 int eegfx_dwt8_operator(double* M) {
   return guarded([&] {
     if (!M) fail(EEGFX_EINVAL, "null argument");

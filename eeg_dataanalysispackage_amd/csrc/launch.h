@@ -75,6 +75,17 @@ struct LrState {
   double w[];
 };
 constexpr int kLrMaxFeatures = 1024;
+
+// plan.hip: marker planning (a4 + a8) as a scan over 3-state balance maps.
+struct PlanResult {
+  int64_t selected;          // accepted markers
+  int64_t balance;           // final class balance
+  int64_t first_unparsable;  // index of the first INT32_MIN stimulus index, -1 if none
+};
+size_t plan_scratch_bytes(int64_t n);
+hipError_t launch_plan_markers(hipStream_t st, const int64_t* pos, const int32_t* stim, int64_t n,
+                               int64_t n_frames, int32_t guessed, int d0, void* scratch,
+                               int64_t* pos_out, double* label_out, PlanResult* result);
 int lr_grid(int64_t n);
 hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrState* state);
 hipError_t launch_lr_iteration(hipStream_t st, const double* X, const double* y, int64_t n, int d,

@@ -144,6 +144,18 @@ int eegfx_plan_markers(const eegfx_marker* markers, int64_t n_markers, int64_t n
                        int32_t guessed, int64_t* balance, int64_t* pos_out, double* label_out,
                        int64_t* n_selected);
 
+/* The same planning on the device, for marker lists of configs[2] size (64M markers): each marker
+ * is a map of the balance state {-1, 0, 1} (target: D <= 0 -> D + 1; non-target: D >= 0 -> D - 1;
+ * out of range: identity), so the sequential walk is a prefix composition, scanned
+ * in parallel, followed by a stream compaction of the accepted markers.  positions /
+ * stimulus_index (INT32_MIN = unparsable description: planning stops there with EEGFX_EFORMAT,
+ * the accepted prefix kept) and pos_out / label_out per `mem`; *balance must be -1, 0 or 1 (the
+ * reference's balance starts at 0 and never leaves that set). */
+int eegfx_plan_markers_device(eegfx_ctx* ctx, const int64_t* positions,
+                              const int32_t* stimulus_index, int64_t n_markers, int64_t n_frames,
+                              int32_t guessed, int64_t* balance, int64_t* pos_out,
+                              double* label_out, int64_t* n_selected, int mem);
+
 /* ---- compute ------------------------------------------------------------------------------ */
 /* a3 + a5..a7: raw multiplexed recording -> baseline-corrected epochs double[n][C][750]
  * (OffLineDataProvider.java:216-233 + EpochHolder.setFZ/CZ/PZ, the List<double[][]> that
