@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "launch.h"
 
@@ -25,6 +26,9 @@ namespace eegfx {
 namespace dev {
 
 constexpr int kLrWaves = 4;
+#ifndef EEGFX_LR_UNROLL
+#define EEGFX_LR_UNROLL 4
+#endif
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -109,11 +113,12 @@ __global__ __launch_bounds__(64 * kLrWaves) void lr_grad16_kernel(
     wv[k] = f < d ? st->w[f] : 0.0;
     acc[k] = 0.0;
   }
-  const int64_t stride = (int64_t)gridDim.x * kLrWaves * 8;
-  for (int64_t r0 = ((int64_t)blockIdx.x * kLrWaves + w) * 8; r0 < n; r0 += stride) {
-    double x[2][FPL], dot[2], yy[2];
+  constexpr int U = EEGFX_LR_UNROLL;  // groups of 4 rows in flight per wave
+  const int64_t stride = (int64_t)gridDim.x * kLrWaves * 4 * U;
+  for (int64_t r0 = ((int64_t)blockIdx.x * kLrWaves + w) * 4 * U; r0 < n; r0 += stride) {
+    double x[U][FPL], dot[U], yy[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t r = r0 + 4 * u + q;
       const bool ok = r < n;
       const double* row = X + (ok ? r : 0) * d;
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(64 * kLrWaves) void lr_grad16_kernel(
       yy[u] = ok ? y[r] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const double m = row16_sum(dot[u]);
       const bool ok = r0 + 4 * u + q < n;
       const double mult = ok ? 1.0 / (1.0 + exp(-m)) - yy[u] : 0.0;
@@ -246,8 +251,12 @@ hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrStat
 }
 
 int lr_grid(int64_t n) {
+  static const int64_t cap = [] {
+    const char* e = getenv("EEGFX_LR_G");
+    return (int64_t)(e ? atoi(e) : 512);
+  }();
   const int64_t g = (n + 16 * dev::kLrWaves - 1) / (16 * dev::kLrWaves);  // >= 16 rows per wave
-  return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
 #define EEGFX_LR_KD(KD, CALL) \
