@@ -185,9 +185,10 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
 
 /* configs[4] -- long recordings streamed from host memory: raw (host, n_frames x
  * n_channels_total samples), pos and features are HOST arrays; the recording is moved to the device
- * in chunks of chunk_frames frames (>= 787, the frames one epoch spans) on a copy stream that
- * overlaps the kernels of the previous chunk (two device chunk buffers; pageable sources go through
- * two pinned staging buffers, pinned sources are copied directly).  Positions may come in any
+ * in chunks of at most chunk_frames frames (>= 787, the frames one epoch spans) on an upload
+ * stream that runs up to three chunks ahead of the kernels (a ring of four device chunk buffers;
+ * pageable sources go through two pinned staging buffers, pinned sources are copied directly),
+ * and the rows of each chunk return on a download stream.  Positions may come in any
  * order; features[i] belongs to pos[i].  Results equal eegfx_process_recording on the whole
  * recording (bit for bit under EEGFX_EXACT).  Replaces the whole-file readBinaryData decode of
  * OffLineDataProvider.java:186-188 for recordings that are not kept resident. */

@@ -65,3 +65,22 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         _lib.lib()
     with pytest.raises(ImportError):
         fx.Context(0)
+
+
+def _build_c_consumer(tmp_path):
+    exe = str(tmp_path / "abi_consumer")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-O1", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "c_abi", "abi_consumer.c"), "-L", libdir, "-leegfx",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    return exe
+
+
+def test_plain_c_consumer(tmp_path):
+    """The ABI from plain C (what the JNI shim is): header parsing, marker planning against the
+    reference golden, error statuses -- no GPU needed."""
+    exe = _build_c_consumer(tmp_path)
+    from conftest import DOD01
+    r = subprocess.run([exe, DOD01], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "abi_consumer ok" in r.stdout
