@@ -168,8 +168,12 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   const int16_t* src = (const int16_t*)((const uint8_t*)(stage + e * G::BSTR) + (tB[e] & 15)) +
                        sel.col[c];
   float b = 0.0f;
+  if constexpr (EEGFX_FUSED_ABLATION & 64) {  // perf study: staging only, no fold
+    b = (float)src[0] * r;
+  } else {
 #pragma unroll 20
-  for (int i = 0; i < kPre; ++i) b = b + (float)src[i * CT] * r;
+    for (int i = 0; i < kPre; ++i) b = b + (float)src[i * CT] * r;
+  }
   if (e < nt) bout[(t0 + e) * C + c] = b / (float)kPre;
 }
 

@@ -42,6 +42,20 @@ int main() {
   (void)hipEventCreate(&b);
   for (int r = 0; r < 2; ++r)
     (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, !getenv("PROBE_EXACT"), base, out);
+  if (getenv("PROBE_BASELINE")) {  // time the baseline kernel instead of the window kernel
+    hipEvent_t c, d;
+    (void)hipEventCreate(&c);
+    (void)hipEventCreate(&d);
+    for (int r = 0; r < 50; ++r) (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
+    (void)hipEventRecord(c);
+    for (int r = 0; r < 500; ++r) (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
+    (void)hipEventRecord(d);
+    (void)hipEventSynchronize(d);
+    float bms;
+    (void)hipEventElapsedTime(&bms, c, d);
+    printf("baseline ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, bms / 500);
+    return 0;
+  }
   const char* it = getenv("PROBE_ITERS");
   const int iters = it ? atoi(it) : 10;
   (void)hipEventRecord(a);
