@@ -55,10 +55,12 @@
 #ifndef EEGFX_HALO0_SHFL
 #define EEGFX_HALO0_SHFL 0
 #endif
-// Decode of the K == 1 kernel: 0 = two samples per packed fp32 op, 1 = one sample per op (72
-// more VALU ops per wave, but 96 instead of 116 VGPRs: 5 waves/SIMD, measured 2 % faster).
+// Decode of the K == 1 kernel: 0 = the whole 72-sample slice decoded up front, two samples per
+// packed fp32 op (116 VGPRs: 4 waves/SIMD); 1 = the same one sample per op (72 more VALU ops per
+// wave, 96 VGPRs: 5 waves/SIMD, 2 % faster than 0); 2 = packed pairs decoded just in time inside
+// level 1 (level1_lds: 94 VGPRs, 5 waves/SIMD, and the 72 VALU ops of 1 saved).
 #ifndef EEGFX_DECODE_SCALAR
-#define EEGFX_DECODE_SCALAR 1
+#define EEGFX_DECODE_SCALAR 2
 #endif
 
 namespace eegfx {
@@ -224,6 +226,30 @@ __device__ __forceinline__ void decode_lds(const int16_t* own, const int16_t* nx
     const f32x2 y = v * rr - bb;
     x[k] = (double)y.x;
     x[k + 1] = (double)y.y;
+  }
+}
+
+// Decode fused into level 1 (EEGFX_DECODE_SCALAR == 2): the samples are decoded two at a time
+// (packed fp32 multiply and subtract: the same two correctly rounded fp32 operations per sample)
+// just before the first level-1 output that needs them, so only the 10-sample sliding window
+// and the level-1 outputs are live -- the packed decode at the register budget of the scalar one.
+template <int CT, bool FAST>
+__device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nxt, float r, float b,
+                                           double (&a1)[40]) {
+  const f32x2 rr = {r, r}, bb = {b, b};
+  double x[kIn];
+#pragma unroll
+  for (int i = 0; i < kIn / 2 - 4; ++i) {  // 32 outputs; output i reads x[2i .. 2i+9]
+#pragma unroll
+    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
+      const int16_t v0 = k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT];
+      const int16_t v1 = k + 1 < kSegLen ? own[(k + 1) * CT] : nxt[(k + 1 - kSegLen) * CT];
+      const f32x2 v = {(float)v0, (float)v1};
+      const f32x2 y = v * rr - bb;
+      x[k] = (double)y.x;
+      x[k + 1] = (double)y.y;
+    }
+    a1[i] = fir10<FAST, false>(x + 2 * i);
   }
 }
 
@@ -462,6 +488,14 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       bcur = (e1 + el < n) ? base[(e1 + el) * C + w] : 0.0f;
       if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane, rows);
     }
+    double a6, d6;
+    if constexpr (K == 1 && EEGFX_DECODE_SCALAR == 2 && !(EEGFX_FUSED_ABLATION & 6) &&
+                  !EEGFX_HALO0_SHFL) {
+      double a1[40];
+      level1_lds<CT, FAST>(own, nxt, r, b, a1);
+      halo<32, SHFL>(a1, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s);
+      dwt8_levels2to6<FAST, SHFL>(a1, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
+    } else {
     double x[kIn];
     if constexpr (EEGFX_FUSED_ABLATION & 2) {
 #pragma unroll
@@ -475,7 +509,6 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     } else {
       decode_pairs(xr, r, b, x);
     }
-    double a6, d6;
     if constexpr (EEGFX_FUSED_ABLATION & 4) {
       a6 = 0.0;
 #pragma unroll
@@ -483,6 +516,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       d6 = a6;
     } else {
       dwt8_cascade<FAST, SHFL>(x, SHFL ? xch : xch + w * 64 * kSlot, lane & ~7, s, a6, d6);
+    }
     }
     double* fb = K > 1 ? feat[kk & 1] : (double*)win;
     if constexpr (K == 1) __syncthreads();  // every wave has read its samples: rows may overwrite
