@@ -55,13 +55,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps; ~50 ms of sustained load brings the clocks to their steady (power-capped) state")
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
-    ap.add_argument("--workload", choices=["c3", "c32", "stream", "logreg"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c32", "stream", "logreg", "svm"], default="c3",
                     help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "
                          "32-channel montage, every channel through the DWT, 512-dim); stream: "
                          "configs[4] (4 h recordings in pinned host memory, a marker every 100 ms, "
                          "streamed to the device in chunks); logreg: the downstream classifier "
                          "(MLlib LogisticRegressionWithSGD, 100 full-batch iterations) on the 1M "
-                         "48-dim feature rows of c3")
+                         "48-dim feature rows of c3; svm: the same with SVMWithSGD")
     ap.add_argument("--chunk-frames", type=int, default=1 << 23, help="stream workload chunk")
     ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
@@ -121,7 +121,7 @@ def main():
 
     if args.workload == "stream":
         return bench_stream(args, rank, world, dev, dist if distributed else None)
-    if args.workload == "logreg":
+    if args.workload in ("logreg", "svm"):
         return bench_logreg(args, rank, world, dev, dist if distributed else None)
     wl = WORKLOADS[args.workload]
     ct, C = wl["ct"], wl["C"]
@@ -368,10 +368,13 @@ def bench_logreg(args, rank, world, dev, dist):
     SGD defaults: 100 iterations, step 1.0, regParam 0.01, full batch) on the device-resident
     feature rows of the c3 workload.  A step = one whole training run; value = rows x iterations
     per second; the roofline is the gradient pass, which reads the n x 48 rows + labels once per
-    iteration."""
+    iteration.  --workload svm: SVMClassifier's SVMWithSGD (HingeGradient), same defaults."""
     import torch
     import eeg_dataanalysispackage_amd as fx
     from eeg_dataanalysispackage_amd import classification as clf
+    svm = args.workload == "svm"
+    train = clf.svm_sgd_train if svm else clf.sgd_train
+    algo = "SVMWithSGD" if svm else "LogisticRegressionWithSGD"
     n = args.epochs
     ctx = fx.Context(dev.index, numerics=args.numerics)
     raw = torch.empty((FRAMES_PER_EPOCH * n + 2000, 3), dtype=torch.int16, device=dev)
@@ -390,8 +393,8 @@ def bench_logreg(args, rank, world, dev, dist):
     iters = clf.DEFAULT_NUM_ITERATIONS
 
     def step():
-        return clf.sgd_train(ctx, X, y, iters, clf.DEFAULT_STEP_SIZE, clf.DEFAULT_REG_PARAM,
-                             clf.DEFAULT_MINI_BATCH_FRACTION, convergence_tol=0.0)
+        return train(ctx, X, y, iters, clf.DEFAULT_STEP_SIZE, clf.DEFAULT_REG_PARAM,
+                     clf.DEFAULT_MINI_BATCH_FRACTION, convergence_tol=0.0)
 
     for _ in range(max(1, min(args.warmup, 5))):
         w, it = step()
@@ -418,25 +421,27 @@ def bench_logreg(args, rank, world, dev, dist):
         k = min(n, 100_000)
         Xh, yh = X[:k].cpu().numpy(), y[:k].cpu().numpy()
         c0 = time.perf_counter()
-        wr, itr = ref.sgd_train(Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0)
+        wr, itr = ref.sgd_train(Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0,
+                                gradient="hinge" if svm else "logistic")
         cdt = time.perf_counter() - c0
-        wg, itg = clf.sgd_train(ctx, Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0)
+        wg, itg = train(ctx, Xh, yh, iters, 1.0, 0.01, convergence_tol=0.0)
         cpu = {"value": round(k * itr / cdt, 1), "unit": "rows*iterations/s", "cores": 1,
                "kind": "port",
                "sample": f"first {k} rows, numpy restatement of MLlib 1.6.2 "
-                         f"LogisticRegressionWithSGD ({itr} iterations, one partition), "
+                         f"{algo} ({itr} iterations, one partition), "
                          f"{cdt:.2f} s wall",
                "gpu_parity_on_sample": bool(np.linalg.norm(wg - wr) <= 1e-9 * np.linalg.norm(wr))}
     if rank == 0:
         print(json.dumps({
-            "metric": "logistic-regression SGD rows*iterations/s (MLlib LogisticRegressionWithSGD, "
-                      "full batch) on the dwt-8 feature rows",
+            "metric": f"{'SVM' if svm else 'logistic-regression'} SGD rows*iterations/s (MLlib "
+                      f"{algo}, full batch) on the dwt-8 feature rows",
             "value": round(world * n * it * steps / elapsed, 1),
             "unit": "rows*iterations/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "logreg: 100 iterations, step 1.0, regParam 0.01 over the c3 "
-                                   "feature rows (1M x 48 per GPU), labels from a fixed direction",
+            "config": {"workload": f"{args.workload}: 100 iterations, step 1.0, regParam 0.01 over "
+                                   "the c3 feature rows (1M x 48 per GPU), labels from a fixed "
+                                   "direction",
                        "rows_per_gpu": n, "features": 48, "iterations": it},
             "roofline": {"bound": "hbm", "achieved": round(bytes_iter / per_iter / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -98,6 +98,11 @@ SIGNATURES = {
                                        POINTER(c_int32), c_int]),
     "eegfx_logreg_predict": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_double,
                                      c_double, c_void_p, c_int]),
+    "eegfx_svm_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                    c_double, c_double, c_double, c_double, c_void_p,
+                                    POINTER(c_int32), c_int]),
+    "eegfx_svm_predict": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_double,
+                                  c_double, c_void_p, c_int]),
     "eegfx_plan_markers_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                           POINTER(c_int64), c_void_p, c_void_p, POINTER(c_int64),
                                           c_int]),

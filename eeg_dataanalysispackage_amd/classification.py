@@ -1,12 +1,15 @@
-"""The downstream classifier of the train/test flow on the GPU.
+"""The downstream classifiers of the train/test flow on the GPU.
 
-Mirrors ``Classification/LogisticRegressionClassifier`` (IClassifier) and
+Mirrors ``Classification/LogisticRegressionClassifier`` and ``Classification/SVMClassifier``
+(IClassifier) and
 ``Utils/ClassificationStatistics`` of the reference: ``train(epochs, targets, fe)`` extracts the
 features of the epochs (one batched device call instead of the Spark map of :90) and fits Spark
 MLlib 1.6.2 ``LogisticRegressionWithSGD`` on the device (``eegfx_logreg_sgd_train``);
 ``test(epochs, targets)`` predicts on the device and builds the statistics exactly as :117-141 do,
 including the reference's reading of the column-major confusion matrix (its "false positives"
-count actual-1 / predicted-0).  Model save/load (Spark model directories) is out of scope.
+count actual-1 / predicted-0).  ``SVMClassifier`` is the same flow with MLlib 1.6.2
+``SVMWithSGD`` (HingeGradient, ``eegfx_svm_sgd_train``) and ``SVMModel.predict`` (margin > 0).
+Model save/load (Spark model directories) is out of scope.
 """
 from __future__ import annotations
 
@@ -27,12 +30,8 @@ DEFAULT_MINI_BATCH_FRACTION = 1.0
 CONVERGENCE_TOL = 0.001
 
 
-def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
-              step_size: float = DEFAULT_STEP_SIZE, reg_param: float = 0.0,
-              mini_batch_fraction: float = DEFAULT_MINI_BATCH_FRACTION,
-              convergence_tol: float = CONVERGENCE_TOL, initial_weights=None):
-    """Full-batch LogisticRegressionWithSGD on the device; returns (weights, iterations_run).
-    X (n x d float64, host numpy or device torch) and y (n labels 0/1) may live on either side."""
+def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini_batch_fraction,
+           convergence_tol, initial_weights):
     if _is_device(X) != _is_device(y):
         raise ValueError("X and y must both be host or both be device arrays")
     if not _is_device(X):
@@ -42,17 +41,13 @@ def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
     w = (np.zeros(d) if initial_weights is None
          else np.array(initial_weights, dtype=np.float64).copy())
     it = c_int32()
-    check(lib().eegfx_logreg_sgd_train(ctx.handle, ptr(X), ptr(y), n, d, int(num_iterations),
-                                       float(step_size), float(reg_param),
-                                       float(mini_batch_fraction), float(convergence_tol),
-                                       ptr(w), byref(it), _mem(X, y)))
+    check(getattr(lib(), entry)(ctx.handle, ptr(X), ptr(y), n, d, int(num_iterations),
+                                float(step_size), float(reg_param), float(mini_batch_fraction),
+                                float(convergence_tol), ptr(w), byref(it), _mem(X, y)))
     return w, it.value
 
 
-def predict(ctx: Context, X, weights, intercept: float = 0.0,
-            threshold: Optional[float] = 0.5):
-    """LogisticRegressionModel.predict on the device: 0/1 per row, or the score when
-    ``threshold`` is None (clearThreshold)."""
+def _predict(entry, ctx: Context, X, weights, intercept, threshold):
     w = np.ascontiguousarray(weights, dtype=np.float64)
     n, d = int(X.shape[0]), int(X.shape[1])
     if _is_device(X):
@@ -62,9 +57,42 @@ def predict(ctx: Context, X, weights, intercept: float = 0.0,
         X = np.ascontiguousarray(X, dtype=np.float64)
         out = np.empty(n, dtype=np.float64)
     t = math.nan if threshold is None else float(threshold)
-    check(lib().eegfx_logreg_predict(ctx.handle, ptr(X), n, d, ptr(w), float(intercept), t,
-                                     ptr(out), _mem(X, out)))
+    check(getattr(lib(), entry)(ctx.handle, ptr(X), n, d, ptr(w), float(intercept), t, ptr(out),
+                                _mem(X, out)))
     return out
+
+
+def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
+              step_size: float = DEFAULT_STEP_SIZE, reg_param: float = 0.0,
+              mini_batch_fraction: float = DEFAULT_MINI_BATCH_FRACTION,
+              convergence_tol: float = CONVERGENCE_TOL, initial_weights=None):
+    """Full-batch LogisticRegressionWithSGD on the device; returns (weights, iterations_run).
+    X (n x d float64, host numpy or device torch) and y (n labels 0/1) may live on either side."""
+    return _train("eegfx_logreg_sgd_train", ctx, X, y, num_iterations, step_size, reg_param,
+                  mini_batch_fraction, convergence_tol, initial_weights)
+
+
+def predict(ctx: Context, X, weights, intercept: float = 0.0,
+            threshold: Optional[float] = 0.5):
+    """LogisticRegressionModel.predict on the device: 0/1 per row, or the score when
+    ``threshold`` is None (clearThreshold)."""
+    return _predict("eegfx_logreg_predict", ctx, X, weights, intercept, threshold)
+
+
+def svm_sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
+                  step_size: float = DEFAULT_STEP_SIZE, reg_param: float = DEFAULT_REG_PARAM,
+                  mini_batch_fraction: float = DEFAULT_MINI_BATCH_FRACTION,
+                  convergence_tol: float = CONVERGENCE_TOL, initial_weights=None):
+    """Full-batch SVMWithSGD (HingeGradient) on the device; returns (weights, iterations_run)."""
+    return _train("eegfx_svm_sgd_train", ctx, X, y, num_iterations, step_size, reg_param,
+                  mini_batch_fraction, convergence_tol, initial_weights)
+
+
+def svm_predict(ctx: Context, X, weights, intercept: float = 0.0,
+                threshold: Optional[float] = 0.0):
+    """SVMModel.predict on the device: margin w.x + b > threshold (0.0) -> 1 else 0, or the
+    margin when ``threshold`` is None (clearThreshold)."""
+    return _predict("eegfx_svm_predict", ctx, X, weights, intercept, threshold)
 
 
 class ClassificationStatistics:
@@ -174,5 +202,35 @@ class LogisticRegressionClassifier:
         return reference_statistics(pred, targets)
 
 
-__all__ = ["ClassificationStatistics", "LogisticRegressionClassifier", "predict",
-           "reference_statistics", "sgd_train", "EegfxError"]
+class SVMClassifier(LogisticRegressionClassifier):
+    """IClassifier for train_clf=svm (SVMClassifier.java), GPU-resident: the same flow as
+    LogisticRegressionClassifier with SVMWithSGD and SVMModel.predict."""
+
+    def train(self, epochs, targets: Sequence[float], fe) -> None:
+        """:83-111 -- with config_num_iterations / config_step_size / config_reg_param /
+        config_mini_batch_fraction all set, the static SVMWithSGD.train(rdd, iterations, step,
+        regParam, fraction); otherwise new SVMWithSGD().run (step 1.0, 100 iterations,
+        regParam 0.01, fraction 1.0)."""
+        self.fe = fe
+        X = self._features(epochs)
+        y = np.asarray(targets, dtype=np.float64)
+        c = self.config
+        if all(k in c for k in ("config_num_iterations", "config_step_size", "config_reg_param",
+                                "config_mini_batch_fraction")):
+            self.weights, self.iterations_run = svm_sgd_train(
+                self.context, X, y, num_iterations=int(c["config_num_iterations"]),
+                step_size=float(c["config_step_size"]), reg_param=float(c["config_reg_param"]),
+                mini_batch_fraction=float(c["config_mini_batch_fraction"]))
+        else:
+            self.weights, self.iterations_run = svm_sgd_train(
+                self.context, X, y, DEFAULT_NUM_ITERATIONS, DEFAULT_STEP_SIZE, DEFAULT_REG_PARAM,
+                DEFAULT_MINI_BATCH_FRACTION)
+
+    def predict(self, features) -> np.ndarray:
+        if self.weights is None:
+            raise RuntimeError("The classifier has not been trained")  # IllegalStateException
+        return svm_predict(self.context, features, self.weights)
+
+
+__all__ = ["ClassificationStatistics", "LogisticRegressionClassifier", "SVMClassifier", "predict",
+           "reference_statistics", "sgd_train", "svm_predict", "svm_sgd_train", "EegfxError"]

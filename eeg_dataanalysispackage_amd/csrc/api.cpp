@@ -857,10 +857,10 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
 // (csrc/logreg.hip): MLlib 1.6.2 LogisticRegressionWithSGD, full batch.  miniBatchFraction < 1
 // samples each partition with Spark's own seeded Bernoulli sampler, which depends on Spark's
 // partitioning -- not reproducible outside Spark, so it is refused.
-int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
-                           int32_t num_iterations, double step_size, double reg_param,
-                           double mini_batch_fraction, double convergence_tol, double* weights,
-                           int32_t* iterations_run, int mem) {
+static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double* y, int64_t n,
+                         int32_t d, int32_t num_iterations, double step_size, double reg_param,
+                         double mini_batch_fraction, double convergence_tol, double* weights,
+                         int32_t* iterations_run, int mem) {
   return guarded([&] {
     if (!ctx || !weights) fail(EEGFX_EINVAL, "null argument");
     check_mem(mem);
@@ -895,8 +895,8 @@ int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int
     const int G = lr_grid(n);
     double* part = (double*)ctx->lr_part.get(sizeof(double) * (size_t)G * d);
     for (int i = 0; i < num_iterations; ++i)
-      HIP_CHECK(launch_lr_iteration(ctx->stream, dX, dy, n, d, st, part, G, step_size, reg_param,
-                                    convergence_tol, num_iterations));
+      HIP_CHECK(launch_lr_iteration(ctx->stream, grad, dX, dy, n, d, st, part, G, step_size,
+                                    reg_param, convergence_tol, num_iterations));
     HIP_CHECK(hipMemcpyAsync(hs.data(), st, sbytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (h->converged == 2) fail(EEGFX_EINVAL, "Input validation failed: labels must be 0.0 or 1.0");
@@ -905,9 +905,9 @@ int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int
   });
 }
 
-int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
-                         const double* weights, double intercept, double threshold, double* out,
-                         int mem) {
+static int glm_predict(int grad, eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
+                       const double* weights, double intercept, double threshold, double* out,
+                       int mem) {
   return guarded([&] {
     if (!ctx || !weights) fail(EEGFX_EINVAL, "null argument");
     check_mem(mem);
@@ -928,14 +928,43 @@ int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
     LrState* st = (LrState*)ctx->lr_state.get(sbytes);
     HIP_CHECK(hipMemcpyAsync(st->w, weights, sizeof(double) * (size_t)d, hipMemcpyHostToDevice,
                              ctx->stream));
-    const bool use_t = !std::isnan(threshold);  // LogisticRegressionModel.clearThreshold -> scores
-    HIP_CHECK(launch_lr_predict(ctx->stream, dX, n, d, st->w, intercept, threshold, use_t ? 1 : 0,
-                                dout));
+    const bool use_t = !std::isnan(threshold);  // clearThreshold -> scores / margins
+    HIP_CHECK(launch_lr_predict(ctx->stream, grad, dX, n, d, st->w, intercept, threshold,
+                                use_t ? 1 : 0, dout));
     if (mem == EEGFX_MEM_HOST)
       HIP_CHECK(hipMemcpyAsync(out, dout, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost,
                                ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
   });
+}
+
+int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
+                           int32_t num_iterations, double step_size, double reg_param,
+                           double mini_batch_fraction, double convergence_tol, double* weights,
+                           int32_t* iterations_run, int mem) {
+  return glm_sgd_train(kGradLogistic, ctx, X, y, n, d, num_iterations, step_size, reg_param,
+                       mini_batch_fraction, convergence_tol, weights, iterations_run, mem);
+}
+
+int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
+                         const double* weights, double intercept, double threshold, double* out,
+                         int mem) {
+  return glm_predict(kGradLogistic, ctx, X, n, d, weights, intercept, threshold, out, mem);
+}
+
+// The classifier of SVMClassifier.java:83-111 (MLlib 1.6.2 SVMWithSGD: HingeGradient, the same
+// SquaredL2Updater / GradientDescent loop) and SVMModel.predict (:71, :114-137).
+int eegfx_svm_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
+                        int32_t num_iterations, double step_size, double reg_param,
+                        double mini_batch_fraction, double convergence_tol, double* weights,
+                        int32_t* iterations_run, int mem) {
+  return glm_sgd_train(kGradHinge, ctx, X, y, n, d, num_iterations, step_size, reg_param,
+                       mini_batch_fraction, convergence_tol, weights, iterations_run, mem);
+}
+
+int eegfx_svm_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d, const double* weights,
+                      double intercept, double threshold, double* out, int mem) {
+  return glm_predict(kGradHinge, ctx, X, n, d, weights, intercept, threshold, out, mem);
 }
 
 int eegfx_plan_markers_device(eegfx_ctx* ctx, const int64_t* positions,

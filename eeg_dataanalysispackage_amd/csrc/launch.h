@@ -88,10 +88,15 @@ hipError_t launch_plan_markers(hipStream_t st, const int64_t* pos, const int32_t
                                int64_t* pos_out, double* label_out, PlanResult* result);
 int lr_grid(int64_t n);
 hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrState* state);
-hipError_t launch_lr_iteration(hipStream_t st, const double* X, const double* y, int64_t n, int d,
-                               LrState* state, double* partial, int G, double step_size,
-                               double reg, double tol, int max_iter);
-hipError_t launch_lr_predict(hipStream_t st, const double* X, int64_t n, int d, const double* w,
-                             double intercept, double threshold, int use_threshold, double* out);
+// grad: kGradLogistic (LogisticRegressionWithSGD) or kGradHinge (SVMWithSGD); the predict
+// kernel scores with the matching model (sigmoid of the margin / the margin itself).
+constexpr int kGradLogistic = 0;
+constexpr int kGradHinge = 1;
+hipError_t launch_lr_iteration(hipStream_t st, int grad, const double* X, const double* y,
+                               int64_t n, int d, LrState* state, double* partial, int G,
+                               double step_size, double reg, double tol, int max_iter);
+hipError_t launch_lr_predict(hipStream_t st, int grad, const double* X, int64_t n, int d,
+                             const double* w, double intercept, double threshold,
+                             int use_threshold, double* out);
 
 }  // namespace eegfx

@@ -17,6 +17,11 @@ The algorithm lives in an un-vendored dependency, ``org.apache.spark:spark-mllib
   when i >= 2 and ||w_prev - w|| < convergenceTol (0.001) * max(||w||, 1).
 * ``LogisticGradient`` (binary): multiplier = 1 / (1 + exp(-w.x)) - label; gradient += multiplier x.
 * ``LogisticRegressionModel.predict``: 1.0 if 1 / (1 + exp(-(w.x + b))) > threshold (0.5).
+* ``SVMClassifier.train`` (Classification/SVMClassifier.java:83-111): ``SVMWithSGD`` -- the same
+  GradientDescent / SquaredL2Updater loop and defaults with ``HingeGradient``: s = 2 label - 1;
+  a row with 1 > s * w.x adds -s x to the gradient, any other row adds nothing (the config_*
+  path passes config_reg_param through).  ``SVMModel.predict`` (:71): 1.0 if w.x + b > threshold
+  (0.0), the margin itself without a threshold.
 * ``test`` (:117-141): MulticlassMetrics' 2x2 confusion matrix (rows = actual label, columns =
   predicted, labels ascending) read through ``toArray`` (column-major) as tn, fp, fn, tp =
   cm[0], cm[1], cm[2], cm[3] -- i.e. the reference's "fp" counts actual-1/predicted-0 and its
@@ -42,8 +47,9 @@ CONVERGENCE_TOL = 0.001
 
 
 def sgd_train(X, y, num_iterations=DEFAULT_ITERS, step_size=DEFAULT_STEP, reg_param=0.0,
-              convergence_tol=CONVERGENCE_TOL, initial=None):
-    """Returns (weights, iterations_run)."""
+              convergence_tol=CONVERGENCE_TOL, initial=None, gradient="logistic"):
+    """Returns (weights, iterations_run).  gradient: "logistic" (LogisticRegressionWithSGD) or
+    "hinge" (SVMWithSGD)."""
     X = np.asarray(X, dtype=np.float64)
     y = np.asarray(y, dtype=np.float64)
     n, d = X.shape
@@ -56,8 +62,12 @@ def sgd_train(X, y, num_iterations=DEFAULT_ITERS, step_size=DEFAULT_STEP, reg_pa
     i = 1
     done = 0
     while i <= num_iterations:
-        margin = -(X @ w)
-        mult = 1.0 / (1.0 + np.exp(margin)) - y
+        if gradient == "hinge":
+            s_lab = 2.0 * y - 1.0
+            mult = np.where(1.0 > s_lab * (X @ w), -s_lab, 0.0)
+        else:
+            margin = -(X @ w)
+            mult = 1.0 / (1.0 + np.exp(margin)) - y
         grad = (mult[:, None] * X).sum(axis=0) / n
         step = step_size / math.sqrt(i)
         w = w * (1.0 - step * reg_param)
@@ -77,6 +87,13 @@ def predict(X, w, intercept=0.0, threshold=0.5):
     if threshold is None:
         return score
     return (score > threshold).astype(np.float64)
+
+
+def svm_predict(X, w, intercept=0.0, threshold=0.0):
+    margin = np.asarray(X, dtype=np.float64) @ w + intercept
+    if threshold is None:
+        return margin
+    return (margin > threshold).astype(np.float64)
 
 
 def reference_statistics(pred, labels):

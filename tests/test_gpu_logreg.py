@@ -111,3 +111,67 @@ def test_classifier_flow_on_info_txt(ctx):
     c.train(data[tr], [labels[i] for i in tr], fe)                 # static train(): regParam 0
     wr, itr = ref.sgd_train(Xtr, ytr, 10, 1.0, 0.0)
     assert c.iterations_run == itr and close(c.weights, wr)
+
+
+# ---- SVMWithSGD (SVMClassifier.java:83-111): the same device loop with HingeGradient ----------
+
+@pytest.mark.parametrize("n,d,reg", [(1, 48, 0.01), (37, 48, 0.0), (5000, 48, 0.01),
+                                     (20000, 48, 0.01), (3000, 512, 0.01), (257, 3, 0.0),
+                                     (100, 1000, 0.0)])
+def test_svm_sgd_matches_mllib_restatement(ctx, n, d, reg):
+    X, y = rows(n, d, 3 * n + d)
+    w, it = clf.svm_sgd_train(ctx, X, y, 100, 1.0, reg)
+    wr, itr = ref.sgd_train(X, y, 100, 1.0, reg, gradient="hinge")
+    assert it == itr
+    assert close(w, wr)
+
+
+def test_svm_device_inputs_and_convergence(ctx):
+    X, y = rows(4000, 48, 17)
+    w, it = clf.svm_sgd_train(ctx, torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), 100,
+                              1.0, 0.01, convergence_tol=0.3)
+    wr, itr = ref.sgd_train(X, y, 100, 1.0, 0.01, convergence_tol=0.3, gradient="hinge")
+    assert 2 <= it == itr < 100
+    assert close(w, wr)
+
+
+def test_svm_predict_and_errors(ctx):
+    X, y = rows(3001, 48, 19)
+    w, _ = ref.sgd_train(X, y, 100, 1.0, 0.01, gradient="hinge")
+    margin = ref.svm_predict(X, w, threshold=None)
+    safe = np.abs(margin) > 1e-9
+    p = clf.svm_predict(ctx, X, w)
+    assert np.array_equal(p[safe], ref.svm_predict(X, w)[safe])
+    m = clf.svm_predict(ctx, X, w, threshold=None)
+    assert np.max(np.abs(m - margin)) <= 1e-12
+    pd = clf.svm_predict(ctx, torch.from_numpy(X).cuda(), w, intercept=0.25)
+    torch.cuda.synchronize()
+    assert np.array_equal(pd.cpu().numpy()[np.abs(margin + 0.25) > 1e-9],
+                          ref.svm_predict(X, w, 0.25)[np.abs(margin + 0.25) > 1e-9])
+    y[5] = -1.0
+    with pytest.raises(fx.EegfxError, match="validation"):
+        clf.svm_sgd_train(ctx, X, y)
+
+
+def test_svm_classifier_flow_on_info_txt(ctx):
+    """ClassifierTest.java:122-145 (train_clf=svm) on the GPU."""
+    odp = fx.OffLineDataProvider([INFO_TRAIN], context=ctx)
+    odp.loadData()
+    fe = fx.WaveletTransform(8, 512, 175, 16, context=ctx)
+    Xtr, ytr, Xte, yte = train_test_features(odp, fe)
+    from eeg_dataanalysispackage_amd.pipeline import reference_split
+    data, labels = odp.getData(), odp.getDataLabels()
+    tr, te = reference_split(len(labels))
+    c = clf.SVMClassifier(context=ctx)
+    with pytest.raises(RuntimeError):
+        c.test(data[te], [labels[i] for i in te])
+    c.train(data[tr], [labels[i] for i in tr], fe)                 # new SVMWithSGD().run()
+    wr, itr = ref.sgd_train(Xtr, ytr, 100, 1.0, 0.01, gradient="hinge")
+    assert c.iterations_run == itr and close(c.weights, wr)
+    stats = c.test(data[te], [labels[i] for i in te])
+    assert stats.as_tuple() == ref.reference_statistics(ref.svm_predict(Xte, wr), yte)
+    c.setConfig({"config_num_iterations": "10", "config_step_size": "0.5",
+                 "config_reg_param": "0.1", "config_mini_batch_fraction": "1.0"})
+    c.train(data[tr], [labels[i] for i in tr], fe)                 # static train(..., regParam)
+    wr, itr = ref.sgd_train(Xtr, ytr, 10, 0.5, 0.1, gradient="hinge")
+    assert c.iterations_run == itr and close(c.weights, wr)

@@ -56,3 +56,27 @@ def test_mllib_restatement_basics():
     # one step from w = 0: multiplier = 0.5 - y; gradient = mean(mult * x)
     g = ((0.5 - y)[:, None] * X).mean(axis=0)
     assert it == 1 and np.allclose(w, -g, rtol=0, atol=1e-16)
+
+
+def test_mllib_hinge_restatement_by_hand():
+    """HingeGradient + SquaredL2Updater, two steps worked by hand (SVMWithSGD defaults)."""
+    import math
+    import numpy as np
+    from oracle import mllib_logreg as ref
+    X = np.array([[1.0, 0.0], [0.0, 1.0], [1.0, 1.0]])
+    y = np.array([1.0, 0.0, 1.0])
+    s = 2 * y - 1
+    # step 1 from w = 0: every row violates (1 > 0), gradient = mean(-s x)
+    g1 = (-s[:, None] * X).mean(axis=0)
+    w1 = np.zeros(2) * (1 - 1.0 * 0.01) - 1.0 * g1
+    w, it = ref.sgd_train(X, y, 1, 1.0, 0.01, gradient="hinge")
+    assert it == 1 and np.array_equal(w, w1)
+    # step 2: only rows with 1 > s * w1.x contribute, step 1/sqrt(2)
+    viol = 1.0 > s * (X @ w1)
+    g2 = np.where(viol[:, None], -s[:, None] * X, 0.0).sum(axis=0) / 3
+    st = 1.0 / math.sqrt(2)
+    w2 = w1 * (1 - st * 0.01) - st * g2
+    w, it = ref.sgd_train(X, y, 2, 1.0, 0.01, convergence_tol=0.0, gradient="hinge")
+    assert it == 2 and np.allclose(w, w2, rtol=0, atol=1e-15)
+    assert np.array_equal(ref.svm_predict(X, w2), (X @ w2 > 0).astype(float))
+    assert np.array_equal(ref.svm_predict(X, w2, threshold=None), X @ w2)

@@ -36,7 +36,7 @@ for NUM in ${NUMS:-fma exact}; do
     --algorithmic-bytes 3476000000 --out "$OUT/traffic_$NUM.json"
 done
 cd "$ROOT"
-for WL in ${EXTRA:-c32 stream logreg}; do
+for WL in ${EXTRA:-c32 stream logreg svm}; do
   echo "== bench $WL"; date
   timeout -k 10 400 python bench.py --workload $WL > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err" || { tail -30 "$OUT/bench_$WL.err"; exit 1; }
   cat "$OUT/bench_$WL.json"
