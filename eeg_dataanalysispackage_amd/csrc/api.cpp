@@ -443,8 +443,6 @@ struct eegfx_odp {
         else if (name == "cz") cz_index = ch.number;
         if (name == "pz") pz_index = ch.number;
       }
-      if (!h.info.multiplexed)
-        fail(EEGFX_ENOTSUP, "%s: VECTORIZED data orientation is not supported", vhdr_file.c_str());
       const int32_t sel[3] = {fz_index, cz_index, pz_index};
       for (int c = 0; c < 3; ++c)
         if (sel[c] < 1 || sel[c] > h.info.n_channels)
@@ -456,7 +454,7 @@ struct eegfx_odp {
       void* d_raw = nullptr;
       if (ctx) {  // planning-only providers (no context) never touch the recording payload
         std::vector<char> host(raw_bytes);
-        read_file_bytes(eeg_file, host.data(), (int64_t)raw_bytes);
+        read_recording(h, eeg_file, host.data(), n_frames);
         d_raw = ctx->raw.get(raw_bytes);
         HIP_CHECK(hipMemcpyAsync(d_raw, host.data(), raw_bytes, hipMemcpyHostToDevice,
                                  ctx->stream));
@@ -591,12 +589,12 @@ int eegfx_read_raw(eegfx_ctx* ctx, const char* vhdr_path, const char* eeg_path, 
     if (bytes > capacity_bytes)
       fail(EEGFX_EINVAL, "capacity %lld < %lld bytes", (long long)capacity_bytes, (long long)bytes);
     if (mem == EEGFX_MEM_HOST) {
-      read_file_bytes(eeg_path, dst, bytes);
+      read_recording(h, eeg_path, dst, n);
     } else {
       if (!ctx) fail(EEGFX_EINVAL, "device read needs a context");
       ctx->activate();
       std::vector<char> host((size_t)bytes);
-      read_file_bytes(eeg_path, host.data(), bytes);
+      read_recording(h, eeg_path, host.data(), n);
       HIP_CHECK(hipMemcpyAsync(dst, host.data(), (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
       HIP_CHECK(hipStreamSynchronize(ctx->stream));
     }

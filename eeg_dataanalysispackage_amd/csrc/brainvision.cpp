@@ -16,6 +16,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <vector>
 
 #include "common.h"
 
@@ -303,6 +304,27 @@ void read_file_bytes(const std::string& path, void* dst, int64_t nbytes) {
   fclose(f);
   if (got != nbytes) fail(EEGFX_EIO, "short read on %s (%lld of %lld bytes)", path.c_str(),
                           (long long)got, (long long)nbytes);
+}
+
+// The recording as multiplexed frames ([n_frames][n_channels] samples), whatever the file's
+// DataOrientation.  A VECTORIZED file stores channel after channel ([n_channels][n_frames]); it is
+// interleaved here, on the host while it is read, so every kernel sees one layout.  eegloader's
+// readBinaryData demultiplexes either orientation to per-channel arrays (OffLineDataProvider.java:
+// 185-188); parity unpinned for VECTORIZED -- no file of the reference's test data uses it.
+void read_recording(const Header& h, const std::string& path, void* dst, int64_t n_frames) {
+  const int64_t sb = sample_bytes(h.info.binary_format), nc = h.info.n_channels;
+  const int64_t nbytes = n_frames * nc * sb;
+  if (h.info.multiplexed) {
+    read_file_bytes(path, dst, nbytes);
+    return;
+  }
+  std::vector<char> v((size_t)nbytes);
+  read_file_bytes(path, v.data(), nbytes);
+  char* out = (char*)dst;
+  for (int64_t c = 0; c < nc; ++c) {
+    const char* src = v.data() + c * n_frames * sb;
+    for (int64_t t = 0; t < n_frames; ++t) memcpy(out + (t * nc + c) * sb, src + t * sb, (size_t)sb);
+  }
 }
 
 }  // namespace eegfx

@@ -67,6 +67,8 @@ int sample_bytes(int32_t binary_format);
 bool file_exists(const std::string& path);
 // Reads the whole .eeg payload (n_frames * n_channels samples) into `dst`.
 void read_file_bytes(const std::string& path, void* dst, int64_t nbytes);
+// n_frames multiplexed frames of the recording (a VECTORIZED file is interleaved on the host).
+void read_recording(const Header& h, const std::string& path, void* dst, int64_t n_frames);
 // Java Integer.parseInt semantics (optional sign, ASCII digits, int32 range); false on failure.
 bool java_parse_int(const std::string& s, int32_t* out);
 // Java String.split(" ") semantics (trailing empty strings removed).

@@ -128,8 +128,9 @@ int eegfx_read_markers(const char* vmrk_path, eegfx_marker* markers, int64_t max
 /* Number of frames of a .eeg file given its header (file size / (channels * sample size)). */
 int eegfx_recording_frames(const char* vhdr_path, const char* eeg_path, int64_t* n_frames);
 /* Reads the raw multiplexed samples of a .eeg file into `dst` (n_frames * n_channels samples of
- * the header's binary format; host or device memory per `mem`).  The decode itself (a3) is done
- * by the kernels, fused with the epoch cut. */
+ * the header's binary format; host or device memory per `mem`).  A DataOrientation=VECTORIZED
+ * file (channel after channel) is interleaved into the same multiplexed layout while it is read.
+ * The decode itself (a3) is done by the kernels, fused with the epoch cut. */
 int eegfx_read_raw(eegfx_ctx* ctx, const char* vhdr_path, const char* eeg_path, void* dst,
                    int64_t capacity_bytes, int mem);
 

@@ -340,3 +340,25 @@ def test_streamed_pinned_source_and_wide_layout(ctx_fma):
     assert np.max(np.abs(got - want)) <= FMA_TOL
     with pytest.raises(fx.EegfxError):
         ctx_fma.process_recording_streamed(raw, ct, cols, [0.1] * 5, pos, chunk_frames=500)
+
+
+def test_vectorized_recording_through_the_provider(ctx, tmp_path):
+    """OffLineDataProvider over a DataOrientation=VECTORIZED copy of DoD2015_01 gives the
+    multiplexed original's epochs and features (parity unpinned against eegloader: the reference's
+    test data holds no VECTORIZED file, so the copy is synthesised)."""
+    raw = fx.read_raw(DOD01 + ".vhdr", DOD01 + ".eeg")
+    vhdr = open(DOD01 + ".vhdr", encoding="utf-8").read()
+    (tmp_path / "DoD2015_01.vhdr").write_text(
+        vhdr.replace("DataOrientation=MULTIPLEXED", "DataOrientation=VECTORIZED"), encoding="utf-8")
+    np.ascontiguousarray(raw.T).tofile(str(tmp_path / "DoD2015_01.eeg"))
+    with open(DOD01 + ".vmrk", "rb") as f:
+        (tmp_path / "DoD2015_01.vmrk").write_bytes(f.read())
+    runs = []
+    for path in (DOD01 + ".eeg", str(tmp_path / "DoD2015_01.eeg")):
+        odp = fx.OffLineDataProvider([path, "1"], context=ctx)
+        odp.loadData()
+        assert odp.last_error == ""
+        runs.append((odp.getData(), odp.getFeatures(), list(odp.getDataLabels())))
+    assert runs[0][0].shape == (11, 3, 750)
+    assert np.array_equal(runs[0][0], runs[1][0]) and eq(runs[0][1], runs[1][1])
+    assert runs[0][2] == runs[1][2]

@@ -201,3 +201,21 @@ def test_dwt8_operator_is_block_circulant():
     for r in range(16):
         row0 = M[8 * (r >> 3)]
         np.testing.assert_allclose(M[r], np.roll(row0, 64 * (r & 7)), rtol=0, atol=1e-15)
+
+
+def test_vectorized_orientation_reads_as_multiplexed(tmp_path):
+    """A DataOrientation=VECTORIZED copy of DoD2015_01 (channel after channel) reads back as the
+    multiplexed original; the planning provider sees the same epochs.  Parity unpinned against
+    eegloader (no VECTORIZED file in the reference's test data): the copy is synthesised here."""
+    raw = fx.read_raw(DOD01 + ".vhdr", DOD01 + ".eeg")
+    vhdr = open(DOD01 + ".vhdr", encoding="utf-8").read()
+    assert "DataOrientation=MULTIPLEXED" in vhdr
+    base = tmp_path / "DoD2015_01"
+    (tmp_path / "DoD2015_01.vhdr").write_text(
+        vhdr.replace("DataOrientation=MULTIPLEXED", "DataOrientation=VECTORIZED"), encoding="utf-8")
+    np.ascontiguousarray(raw.T).tofile(str(base) + ".eeg")
+    with open(DOD01 + ".vmrk", "rb") as f:
+        (tmp_path / "DoD2015_01.vmrk").write_bytes(f.read())
+    assert fx.read_header(str(base) + ".vhdr").multiplexed is False
+    back = fx.read_raw(str(base) + ".vhdr", str(base) + ".eeg")
+    assert back.dtype == raw.dtype and np.array_equal(back, raw)
