@@ -35,6 +35,9 @@ def bytes_per_epoch(ct, C):
     (3 ch: 4,064 B; 32 ch: 43,272 B)."""
     return 612 * ct * 2 + 8 + 16 * C * 8
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VECTOR_PEAK_TFS = 78.6                    # vendor fp64 vector spec (SURVEY.md 8d; not in the guide)
+FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01b_perf_study.json)
+FLOP_PER_SIGNAL = 2 * 5120                     # SURVEY.md 8d: minimal a-path cascade, per channel
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
 WINDOW_KERNEL = {"exact": "window_kernel<int16,3>", "fma": "window_kernel<int16,3>",
@@ -95,6 +98,18 @@ def traffic_from_profiles(workload_key):
             if d.get("workload_key") == workload_key and d.get("hbm_bytes_per_launch"):
                 best = d
     return best
+
+
+def valu_issue_from_profiles(applies):
+    """VALU issue share of window_kernel's cycles (SQ_INSTS_VALU x 4 / SIMD cycles at the
+    effective clock) from the committed counter pass; None for kernels it was not measured on."""
+    if not applies:
+        return None
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "r01j_pmc_window_fma.json")))
+        return d["derived"]["valu_issue_utilisation"]
+    except Exception:
+        return None
 
 
 def main():
@@ -268,6 +283,18 @@ def main():
                 "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": bpe,
                                "GBps": round(path_gbs, 1),
                                "frac": round(path_gbs / HBM_PEAK_GBS, 4)},
+                # the other side of the kernel's balance: fp64 filter-bank flops
+                # (5,120 MAC per signal) against the vector fp64 peak, and the VALU issue share
+                # of the kernel's cycles from the committed SQ counter pass
+                "fp64": {"flop_per_epoch": FLOP_PER_SIGNAL * C,
+                         "achieved_TFs": round(FLOP_PER_SIGNAL * C * n / (kernel_ms * 1e-3) / 1e12, 2),
+                         "peak_TFs": FP64_VECTOR_PEAK_TFS,
+                         "measured_fma_peak_TFs": FP64_FMA_MEASURED_TFS,
+                         "frac": round(FLOP_PER_SIGNAL * C * n / (kernel_ms * 1e-3) / 1e12
+                                       / FP64_VECTOR_PEAK_TFS, 4),
+                         "valu_issue_utilisation": valu_issue_from_profiles(
+                             C == 3 and args.numerics == "fma"),
+                         "source": "profiles/r01j_pmc_window_fma.json (fma, c3)"},
             },
             "cpu_baseline": cpu,
         }
