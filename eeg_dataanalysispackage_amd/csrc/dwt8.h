@@ -172,6 +172,28 @@ __device__ __forceinline__ void dwt8_levels2to6(double (&a1)[40], double* xch, i
   d6 = fir10<FAST, true>(a5);
 }
 
+// Level 1 with the decode (DataProviderUtils.java:49-59, Baseline.java:39-41: (double)((float)v *
+// res - b), two correctly rounded fp32 operations) fused in: samples are fetched and decoded two
+// at a time with packed fp32 math just before the first output that needs them, so only a
+// 10-sample window and the outputs are live.  fetch(k) returns sample k (k < 72) as float.
+typedef float dwt8_f32x2 __attribute__((ext_vector_type(2)));
+template <bool FAST, typename Fetch>
+__device__ __forceinline__ void level1_jit(Fetch fetch, float r, float b, double (&a1)[40]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  double x[kIn];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {  // output i reads x[2i .. 2i+9]
+#pragma unroll
+    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
+      const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
+      const dwt8_f32x2 y = v * rr - bb;
+      x[k] = (double)y.x;
+      x[k + 1] = (double)y.y;
+    }
+    a1[i] = fir10<FAST, false>(x + 2 * i);
+  }
+}
+
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
 // xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
 // Returns a6[s] and d6[s].

@@ -124,14 +124,16 @@ __device__ __forceinline__ float sample_at(const uint8_t* p) {
 }
 
 // Per-workgroup LDS: EPW epochs x 8 segment blocks of SEGQ quads, then EPW x F features, then
-// EPW norms.  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame.
-template <typename T, bool FAST, int EPW>
+// EPW norms.  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame; FBC != 0 fixes FB at compile
+// time (configs[3]'s 32-channel int16 montage: 64), so every sample read of the decode is an
+// immediate LDS offset instead of an address computed per sample.
+template <typename T, bool FAST, int EPW, int FBC = 0>
 __global__ __launch_bounds__(256) void window_wide_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
     const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
     double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int FB = ct * (int)sizeof(T);
+  const int FB = FBC ? FBC : ct * (int)sizeof(T);
   const int SEGQ = 4 * FB + 1;
   const int EQ = 8 * SEGQ;
   const int F = 16 * C;
@@ -192,13 +194,12 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
     const float r = sel.res[c];
     const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
-    double x[kIn];
-#pragma unroll
-    for (int k = 0; k < kSegLen; ++k) x[k] = (double)(sample_at<T>(own + k * FB) * r - b);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[kSegLen + k] = (double)(sample_at<T>(nxt + k * FB) * r - b);
-    double a6, d6;
-    dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
+    double a1[40], a6, d6;
+    level1_jit<FAST>(
+        [&](int k) { return sample_at<T>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
+        r, b, a1);
+    halo<32, true>(a1, nullptr, lane & ~7, s);
+    dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
     if (valid) {
       feat[m * F + c * 16 + s] = a6;
       feat[m * F + c * 16 + 8 + s] = d6;
@@ -234,14 +235,14 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
 }  // namespace dev
 
 namespace {
-template <typename T, bool FAST, int EPW>
+template <typename T, bool FAST, int EPW, int FBC = 0>
 hipError_t launch_wide_t(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                          const ChanSel& sel, int C, const int64_t* pos, const float* base,
                          int64_t n, double* out) {
   const int FB = ct * (int)sizeof(T);
   const size_t lds = (size_t)EPW * 8 * (4 * FB + 1) * 16 + (size_t)EPW * 16 * C * 8 + EPW * 8;
   const dim3 grid((unsigned)((n + EPW - 1) / EPW));
-  hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW>), grid, dim3(256), lds, st,
+  hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW, FBC>), grid, dim3(256), lds, st,
                      (const uint8_t*)raw, n_frames, ct, sel, C, pos, base, n, out);
   return hipGetLastError();
 }
@@ -301,6 +302,10 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
 #define EEGFX_W(T, FA)                                                                        \
   return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out)       \
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
+  if (fmt == 0 && ct == 32 && !two) {  // configs[3]: the frame size as a compile-time constant
+    return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
+                : launch_wide_t<int16_t, false, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
+  }
   if (fmt == 0) {
     if (fast) { EEGFX_W(int16_t, true) } else { EEGFX_W(int16_t, false) }
   } else {
