@@ -226,7 +226,8 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   }
   if (fused_supported(fmt, ct, C, out)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
-    HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch));
+    if (!fused_baseline_in_window())
+      HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch));
     ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
     HIP_CHECK(launch_fused_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fast, fscratch,
                                   out));

@@ -422,12 +422,56 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
   }
 }
 
+// The baseline of (epoch first+el, channel col) inside the window kernel (FUSEB): a3 + a5 + a6's
+// prefix, Baseline.java:29-42, without the separate baseline_kernel pass.  The 8 lanes of an
+// epoch group (s = 0..7) each load and scale a 13-sample chunk of the 100 pre-stimulus frames
+// ((float)raw * res, one rounded fp32 multiply; frames outside the recording are the reference's
+// +0.0f padding), then fold them in sample order as ONE sequential chain: stage k adds lane k's
+// chunk to the running sum and hands it to lane k+1 -- the exact operation sequence of the
+// reference's loop.  Returns b / 100 in every lane of the group.  The loads are issued before the
+// window DMAs, so the chain waits only as long as the window does.
+template <int CT>
+__device__ __forceinline__ void fused_baseline_load(const uint8_t* __restrict__ raw, int64_t n_frames,
+                                                    const int64_t* __restrict__ pos, int64_t n,
+                                                    int64_t first, int el, int s, int col, float r,
+                                                    float (&p)[13]) {
+  constexpr int CH = 13;
+  const int64_t nbytes = n_frames * 2 * CT;
+  const int64_t e = first + el < n ? first + el : n - 1;
+  const int64_t f0 = pos[e] - kPre + CH * s;
+  const int16_t* placeholder = (const int16_t*)safe_quad(raw, nbytes);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int64_t f = f0 + j;
+    const bool in = CH * s + j < kPre && f >= 0 && f < n_frames;
+    const int16_t v = *(in ? (const int16_t*)raw + f * CT + col : placeholder);
+    p[j] = in ? (float)v * r : 0.0f;
+  }
+}
+__device__ __forceinline__ float fused_baseline_fold(const float (&p)[13], int lane, int s) {
+  constexpr int CH = 13;
+  float acc = 0.0f;
+#pragma unroll
+  for (int stage = 0; stage < 8; ++stage) {
+    if (s == stage) {
+#pragma unroll
+      for (int j = 0; j < (stage < 7 ? CH : kPre - 7 * CH); ++j) acc = acc + p[j];
+    }
+    if (stage < 7) {
+      const float prev = __shfl(acc, (lane & ~7) | stage, 64);
+      if (s == stage + 1) acc = prev;
+    }
+  }
+  const float b = __shfl(acc, lane | 7, 64);
+  return b / (float)kPre;
+}
+
 // LDS-DMA pipeline: the window of sub-tile k+1 is fetched by global_load_lds_dwordx4 (16-byte
 // aligned per-lane sources, dword-aligned contiguous LDS destinations, no VGPRs) into the single
 // window buffer as soon as every lane has copied its raw samples of sub-tile k into registers;
 // the transfer overlaps the whole filter bank.  K sub-tiles per workgroup, unrolled; the barrier
 // that publishes the features of sub-tile k also publishes the window of k+1.
-template <int CT, int C, bool FAST, int MINW, int K, bool SHFL = true>
+template <int CT, int C, bool FAST, int MINW, int K, bool SHFL = true, bool FUSEB = false>
 __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
     const float* __restrict__ base, int64_t n, double* __restrict__ out) {
@@ -450,10 +494,14 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
 
   if (w == 0 && lane < kSub)
     tdelta[0][lane] = first + lane < n ? (int)(window_byte<CT>(pos, first + lane) & 15) : 0;
-  float bcur = (first + el < n) ? base[(first + el) * C + w] : 0.0f;
+  static_assert(!FUSEB || K == 1, "in-kernel baselines: one sub-tile per workgroup");
+  float bp[13];
+  if constexpr (FUSEB) fused_baseline_load<CT>(raw, n_frames, pos, n, first, el, s, col, r, bp);
+  float bcur = FUSEB ? 0.0f : ((first + el < n) ? base[(first + el) * C + w] : 0.0f);
   const DmaRows<CT> rows(lane);
   if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows))
     dma_fixup<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows);
+  if constexpr (FUSEB) bcur = fused_baseline_fold(bp, lane, s);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
@@ -943,6 +991,16 @@ __global__ __launch_bounds__(64 * (L + G_ * C), 1) void engine_kernel(
 }
 }  // namespace dev
 
+// Baselines folded inside window_kernel (FUSEB, one launch per batch) instead of by the
+// baseline_kernel pass before it.  EEGFX_FUSE_BASELINE=0/1 overrides the default.
+bool fused_baseline_in_window() {
+  static const bool v = [] {
+    const char* e = getenv("EEGFX_FUSE_BASELINE");
+    return e ? e[0] == '1' : false;
+  }();
+  return v;
+}
+
 namespace {
 // Variant selector (perf study): EEGFX_FUSED_IMPL = "<d|l><minw><K>": d = cross-lane
 // (ds_bpermute) halos, l = LDS-slot halos; minw = launch-bounds waves per EU; K = sub-tiles per
@@ -971,6 +1029,11 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
                     const int64_t* pos, const float* base, int64_t n, double* out) {
   const Impl im = impl_choice();
   const int64_t nsub = (n + dev::kSub - 1) / dev::kSub;
+  if (fused_baseline_in_window()) {
+    hipLaunchKernelGGL((dev::window_kernel<3, 3, FAST, 4, 1, true, true>), dim3((unsigned)nsub),
+                       dim3(192), 0, st, (const uint8_t*)raw, n_frames, sel, pos, nullptr, n, out);
+    return;
+  }
   const dim3 g((unsigned)((nsub + im.k - 1) / im.k));
   bool launched = false;
 #define EEGFX_D(MW, KK, SH)                                                                       \
@@ -1031,7 +1094,10 @@ bool fused_supported(int fmt, int ct, int C, const double* out) {
 size_t fused_scratch_bytes(int64_t n, int C) { return sizeof(float) * (size_t)n * (size_t)C; }
 
 int64_t fused_window_bytes_per_epoch(int ct, int C) {
-  return (int64_t)dev::kWin * ct * 2 + (int64_t)C * 4 + 8 + (int64_t)C * 16 * 8;
+  // window + (12 B of baselines | the 100 pre-stimulus frames when folded in the kernel) +
+  // position + feature row
+  const int64_t b = fused_baseline_in_window() ? (int64_t)dev::kPre * ct * 2 : (int64_t)C * 4;
+  return (int64_t)dev::kWin * ct * 2 + b + 8 + (int64_t)C * 16 * 8;
 }
 
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,

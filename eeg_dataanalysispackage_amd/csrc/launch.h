@@ -41,6 +41,9 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
 // Algorithmic HBM bytes per epoch of window_kernel (the dominant kernel): window frames, the
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);
+// True when window_kernel folds the baselines itself (then launch_fused_baseline is skipped and
+// launch_fused_window ignores `scratch`).
+bool fused_baseline_in_window();
 
 // Any-layout fused path (wide.hip): baseline_any_kernel then window_wide_kernel, same scratch
 // contract as the 3-channel kernels.  wide_supported: int16/float32, C <= 64, one epoch's staged
