@@ -365,7 +365,7 @@ struct DmaRows {
 // DMA, so the DMAs leave back to back; an epoch whose whole window lies inside the recording (a
 // scalar test) takes the unguarded path.  Returns whether some in-range quad of this lane could
 // not be DMA'd (the recording ends inside the window).
-template <int CT, int C>
+template <int CT, int C, bool NT = false>
 __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
                                           const int64_t* __restrict__ pos, int64_t n, int64_t e0,
                                           uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
@@ -389,12 +389,12 @@ __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64
     if (Bq[t] + kSpanB <= nbytes) {
 #pragma unroll
       for (int j = 0; j < PER_E; ++j)
-        if (64 * (j + 1) <= G::EPQ || 64 * j + lane < G::EPQ) dma16_s(sb, rows.off[j], dst + 256 * j);
+        if (64 * (j + 1) <= G::EPQ || 64 * j + lane < G::EPQ) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
     } else {
 #pragma unroll
       for (int j = 0; j < PER_E; ++j) {
         if (64 * j + lane >= G::EPQ) continue;
-        if (Bq[t] + rows.off[j] + 16 <= nbytes) dma16_s(sb, rows.off[j], dst + 256 * j);
+        if (Bq[t] + rows.off[j] + 16 <= nbytes) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
         else need_fix = true;
       }
     }
@@ -471,7 +471,8 @@ __device__ __forceinline__ float fused_baseline_fold(const float (&p)[13], int l
 // window buffer as soon as every lane has copied its raw samples of sub-tile k into registers;
 // the transfer overlaps the whole filter bank.  K sub-tiles per workgroup, unrolled; the barrier
 // that publishes the features of sub-tile k also publishes the window of k+1.
-template <int CT, int C, bool FAST, int MINW, int K, bool SHFL = true, bool FUSEB = false>
+template <int CT, int C, bool FAST, int MINW, int K, bool SHFL = true, bool FUSEB = false,
+          bool NT = false>
 __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
     const float* __restrict__ base, int64_t n, double* __restrict__ out) {
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
   if constexpr (FUSEB) fused_baseline_load<CT>(raw, n_frames, pos, n, first, el, s, col, r, bp);
   float bcur = FUSEB ? 0.0f : ((first + el < n) ? base[(first + el) * C + w] : 0.0f);
   const DmaRows<CT> rows(lane);
-  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows))
+  if (!(EEGFX_FUSED_ABLATION & 1) && dma_issue<CT, C, NT>(raw, nbytes, pos, n, first, win, w, lane, rows))
     dma_fixup<CT, C>(raw, nbytes, pos, n, first, win, w, lane, rows);
   if constexpr (FUSEB) bcur = fused_baseline_fold(bp, lane, s);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -534,7 +535,7 @@ __global__ __launch_bounds__(64 * C, MINW) void window_kernel(
       if (w == 0 && lane < kSub)
         tdelta[(kk + 1) & 1][lane] = e1 + lane < n ? (int)(window_byte<CT>(pos, e1 + lane) & 15) : 0;
       bcur = (e1 + el < n) ? base[(e1 + el) * C + w] : 0.0f;
-      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C>(raw, nbytes, pos, n, e1, win, w, lane, rows);
+      if (!(EEGFX_FUSED_ABLATION & 1)) need_fix = dma_issue<CT, C, NT>(raw, nbytes, pos, n, e1, win, w, lane, rows);
     }
     double a6, d6;
     if constexpr (K == 1 && EEGFX_DECODE_SCALAR == 2 && !(EEGFX_FUSED_ABLATION & 6) &&
@@ -1034,9 +1035,23 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
                        dim3(192), 0, st, (const uint8_t*)raw, n_frames, sel, pos, nullptr, n, out);
     return;
   }
+  // Non-temporal window reads when the windows (512 frames) of neighbouring markers do not
+  // overlap on average, i.e. no window shares its bytes with another through L2 (lds_dma.h has
+  // the measurements).  EEGFX_DMA_NT=0/1 overrides.
+  static const int nt_env = [] {
+    const char* e = getenv("EEGFX_DMA_NT");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  const bool nt = nt_env >= 0 ? nt_env == 1 : n_frames / n >= dev::kWin + 8;
+  if (nt && im.minw == 4 && im.k == 1 && im.shfl) {
+    hipLaunchKernelGGL((dev::window_kernel<3, 3, FAST, 4, 1, true, false, true>),
+                       dim3((unsigned)nsub), dim3(192), 0, st, (const uint8_t*)raw, n_frames, sel,
+                       pos, base, n, out);
+    return;
+  }
   const dim3 g((unsigned)((nsub + im.k - 1) / im.k));
   bool launched = false;
-#define EEGFX_D(MW, KK, SH)                                                                       \
+#define EEGFX_D(MW, KK, SH)                                                                     \
   if (!launched && im.minw == MW && im.k == KK && im.shfl == SH) {                                \
     hipLaunchKernelGGL((dev::window_kernel<3, 3, FAST, MW, KK, SH>), g, dim3(192), 0, st,          \
                        (const uint8_t*)raw, n_frames, sel, pos, base, n, out);                    \
