@@ -46,9 +46,9 @@
 #endif
 // FMA-mode row store: 0 = each lane stores its own 6 normalised features (16-byte pieces 48 bytes
 // apart), 1 = rows staged back into LDS and stored as contiguous 1 KB wave stores, 2 = as 1 with
-// non-temporal stores.
+// non-temporal stores (0.928 -> 0.924 ms in tools/probes, twice; the default).
 #ifndef EEGFX_STORE_MODE
-#define EEGFX_STORE_MODE 1
+#define EEGFX_STORE_MODE 2
 #endif
 // Level-0 halo: 0 = every lane decodes its 8 halo samples from LDS, 1 = lanes decode only their
 // 64 own samples and take the halo (8 doubles) from lane s+1 through ds_bpermute.
@@ -59,6 +59,9 @@
 // packed fp32 op (116 VGPRs: 4 waves/SIMD); 1 = the same one sample per op (72 more VALU ops per
 // wave, 96 VGPRs: 5 waves/SIMD, 2 % faster than 0); 2 = packed pairs decoded just in time inside
 // level 1 (level1_lds: 94 VGPRs, 5 waves/SIMD, and the 72 VALU ops of 1 saved).
+#ifndef EEGFX_BASELINE_NT
+#define EEGFX_BASELINE_NT 0
+#endif
 #ifndef EEGFX_DECODE_SCALAR
 #define EEGFX_DECODE_SCALAR 2
 #endif
@@ -114,10 +117,16 @@ __device__ __forceinline__ u32x4_a4 load16(const uint8_t* __restrict__ raw, int6
 // lane reads the first quad of the recording and discards it), so the compiler batches every
 // load of a thread before the first wait; the rare quad that straddles the end of the recording
 // is patched afterwards by load16.
+// NT: non-temporal read, for pre-stimulus frames no other epoch's window or baseline shares
+// (baseline_kernel 0.136 -> 0.124 ms with markers 1,000 frames apart, tools/probes).
+template <bool NT = false>
 __device__ __forceinline__ u32x4_a4 load16_bulk(const uint8_t* __restrict__ raw, int64_t nbytes,
                                                 int64_t A, bool want) {
   const bool full = want && A >= 0 && A + 16 <= nbytes;
-  const u32x4_a4 v = *(const u32x4_a16*)(full ? raw + A : safe_quad(raw, nbytes));
+  const u32x4_a16* src = (const u32x4_a16*)(full ? raw + A : safe_quad(raw, nbytes));
+  u32x4_a4 v;
+  if constexpr (NT || EEGFX_BASELINE_NT) v = __builtin_nontemporal_load(src);
+  else v = *src;
   const u32x4_a4 z = {0u, 0u, 0u, 0u};
   return full ? v : z;
 }
@@ -125,7 +134,7 @@ __device__ __forceinline__ bool straddles_end(int64_t A, int64_t nbytes, bool wa
   return want && A >= 0 && A < nbytes && A + 16 > nbytes;
 }
 
-template <int CT, int C, int TILE>
+template <int CT, int C, int TILE, bool STREAM = false>
 __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
     int64_t n, float* __restrict__ bout) {
@@ -150,7 +159,7 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const int e = i / G::BASEQ, q = i - e * G::BASEQ;
     want[k] = i < TILE * G::BASEQ && e < nt;
     A[k] = want[k] ? (tB[e] & ~(int64_t)15) + 16 * q : 0;
-    v[k] = load16_bulk(raw, nbytes, A[k], want[k] && !tiny);
+    v[k] = load16_bulk<STREAM>(raw, nbytes, A[k], want[k] && !tiny);
   }
 #pragma unroll
   for (int k = 0; k < ITERS; ++k)
@@ -1002,6 +1011,17 @@ bool fused_baseline_in_window() {
   return v;
 }
 
+// Non-temporal (streaming) reads when the average marker spacing n_frames / n leaves the regions
+// a kernel reads (min_spacing frames per epoch) disjoint, so no other epoch would reuse the bytes
+// through L2.  EEGFX_DMA_NT=0/1 overrides.
+static bool streaming_reads(int64_t n_frames, int64_t n, int64_t min_spacing) {
+  static const int env = [] {
+    const char* e = getenv("EEGFX_DMA_NT");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return env >= 0 ? env == 1 : (n > 0 && n_frames / n >= min_spacing);
+}
+
 namespace {
 // Variant selector (perf study): EEGFX_FUSED_IMPL = "<d|l><minw><K>": d = cross-lane
 // (ds_bpermute) halos, l = LDS-slot halos; minw = launch-bounds waves per EU; K = sub-tiles per
@@ -1035,14 +1055,9 @@ void launch_window3(hipStream_t st, const void* raw, int64_t n_frames, const Cha
                        dim3(192), 0, st, (const uint8_t*)raw, n_frames, sel, pos, nullptr, n, out);
     return;
   }
-  // Non-temporal window reads when the windows (512 frames) of neighbouring markers do not
-  // overlap on average, i.e. no window shares its bytes with another through L2 (lds_dma.h has
-  // the measurements).  EEGFX_DMA_NT=0/1 overrides.
-  static const int nt_env = [] {
-    const char* e = getenv("EEGFX_DMA_NT");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
-  const bool nt = nt_env >= 0 ? nt_env == 1 : n_frames / n >= dev::kWin + 8;
+  // Non-temporal window reads when the 512-frame windows of neighbouring markers do not overlap
+  // (lds_dma.h has the measurements).
+  const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
   if (nt && im.minw == 4 && im.k == 1 && im.shfl) {
     hipLaunchKernelGGL((dev::window_kernel<3, 3, FAST, 4, 1, true, false, true>),
                        dim3((unsigned)nsub), dim3(192), 0, st, (const uint8_t*)raw, n_frames, sel,
@@ -1120,9 +1135,15 @@ hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_fram
                                  void* scratch) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
-  // 64 epochs per workgroup; 16/32/128 measured the same or slower
-  hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), dim3((unsigned)((n + 63) / 64)), dim3(192),
-                     0, st, (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch);
+  // 64 epochs per workgroup; 16/32/128 measured the same or slower.  Streaming
+  // reads unless another epoch's window or baseline may share the pre-stimulus frames.
+  const dim3 g((unsigned)((n + 63) / 64));
+  if (streaming_reads(n_frames, n, dev::kPre + 687))
+    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,
+                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch);
+  else
+    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,
+                       n_frames, sel, pos, n, (float*)scratch);
   return hipGetLastError();
 }
 
