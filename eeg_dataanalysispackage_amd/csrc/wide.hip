@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "dwt8.h"
 #include "launch.h"
@@ -127,7 +128,7 @@ __device__ __forceinline__ float sample_at(const uint8_t* p) {
 // EPW norms.  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame; FBC != 0 fixes FB at compile
 // time (configs[3]'s 32-channel int16 montage: 64), so every sample read of the decode is an
 // immediate LDS offset instead of an address computed per sample.
-template <typename T, bool FAST, int EPW, int FBC = 0>
+template <typename T, bool FAST, int EPW, int FBC = 0, bool STREAM = false>
 __global__ __launch_bounds__(256) void window_wide_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
     const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
       uint8_t* dst = win + ((size_t)m * EQ + 64 * j) * 16;
       if (i < EQ) {
         if (full || Bq[m] + off + 16 <= nbytes) {
-          dma16_s(sb, off, dst);
+          dma16_s<STREAM>(sb, off, dst);
         } else {
           const wq_a4 v = wide_load16(raw, nbytes, Bq[m] + off);
           uint32_t* d = (uint32_t*)(dst + 16 * lane);
@@ -229,20 +230,24 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   }
   __syncthreads();
   double* o = out + e0 * F;
-  for (int i = tid; i < ne * F; i += blockDim.x) o[i] = feat[i] / norm[i / F];
+  for (int i = tid; i < ne * F; i += blockDim.x) {
+    const double v = feat[i] / norm[i / F];
+    if constexpr (STREAM) __builtin_nontemporal_store(v, o + i);
+    else o[i] = v;
+  }
 }
 
 }  // namespace dev
 
 namespace {
-template <typename T, bool FAST, int EPW, int FBC = 0>
+template <typename T, bool FAST, int EPW, int FBC = 0, bool STREAM = false>
 hipError_t launch_wide_t(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                          const ChanSel& sel, int C, const int64_t* pos, const float* base,
                          int64_t n, double* out) {
   const int FB = ct * (int)sizeof(T);
   const size_t lds = (size_t)EPW * 8 * (4 * FB + 1) * 16 + (size_t)EPW * 16 * C * 8 + EPW * 8;
   const dim3 grid((unsigned)((n + EPW - 1) / EPW));
-  hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW, FBC>), grid, dim3(256), lds, st,
+  hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW, FBC, STREAM>), grid, dim3(256), lds, st,
                      (const uint8_t*)raw, n_frames, ct, sel, C, pos, base, n, out);
   return hipGetLastError();
 }
@@ -293,6 +298,16 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
   return hipGetLastError();
 }
 
+// Same test as the c3 kernels (fused.hip streaming_reads): the 512-frame windows of neighbouring
+// markers are disjoint on average; EEGFX_DMA_NT=0/1 overrides.
+static bool wide_streaming(int64_t n_frames, int64_t n) {
+  static const int env = [] {
+    const char* e = getenv("EEGFX_DMA_NT");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return env >= 0 ? env == 1 : (n > 0 && n_frames / n >= dev::kWin + 8);
+}
+
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
                               const void* scratch, double* out) {
@@ -303,6 +318,10 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
   return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out)       \
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
   if (fmt == 0 && ct == 32 && !two) {  // configs[3]: the frame size as a compile-time constant
+    // streaming (non-temporal) window reads and row stores when the windows are disjoint
+    if (wide_streaming(n_frames, n))
+      return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
+                  : launch_wide_t<int16_t, false, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
     return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
                 : launch_wide_t<int16_t, false, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
   }
