@@ -35,7 +35,7 @@ typedef uint32_t wq_a16 __attribute__((ext_vector_type(4), aligned(16)));
 // consecutive blocks by 4 banks), then lane (epoch, selected channel) folds its 100 samples from
 // LDS.  Quads outside the recording are staged as zeros, which is the reference's zero padding
 // for the fold (a padded +0.0f adds nothing, and the running sum is never -0.0f).
-template <typename T>
+template <typename T, bool STREAM = false>
 __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __restrict__ raw,
                                                            int64_t n_frames, int ct, ChanSel sel,
                                                            int C, const int64_t* __restrict__ pos,
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
     if (q < NQ) {
       const int64_t A = Bq + 16 * q;
       if (full || (A >= 0 && A + 16 <= nbytes)) {
-        dma16_s(raw + Bq, (uint32_t)(16 * q), dst);
+        dma16_s<STREAM>(raw + Bq, (uint32_t)(16 * q), dst);
       } else {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (A + 16 > 0 && A < nbytes) {  // the recording starts or ends inside this quad
@@ -281,6 +281,16 @@ bool baseline_any_supported(int fmt, int ct, int C) {
   return (size_t)EB * bstq * 16 <= 64 * 1024;
 }
 
+// Same test as the c3 kernels (fused.hip streaming_reads): the regions a kernel reads (min_spacing
+// frames per epoch) of neighbouring markers are disjoint on average; EEGFX_DMA_NT=0/1 overrides.
+static bool wide_streaming(int64_t n_frames, int64_t n, int64_t min_spacing) {
+  static const int env = [] {
+    const char* e = getenv("EEGFX_DMA_NT");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return env >= 0 ? env == 1 : (n > 0 && n_frames / n >= min_spacing);
+}
+
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                                void* scratch) {
@@ -289,23 +299,16 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
   const int EB = baseline_any_tile(fmt, ct, C, &BSTQ);
   const size_t lds = (size_t)EB * BSTQ * 16;
   const dim3 grid((unsigned)((n + EB - 1) / EB));
-  if (fmt == 0)
+  if (fmt == 0 && wide_streaming(n_frames, n, dev::kPre + 687))  // pre-stimulus frames unshared
+    hipLaunchKernelGGL((dev::baseline_any_kernel<int16_t, true>), grid, dim3(256), lds, st,
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
+  else if (fmt == 0)
     hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), lds, st,
                        (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
   else
     hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), lds, st,
                        (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
   return hipGetLastError();
-}
-
-// Same test as the c3 kernels (fused.hip streaming_reads): the 512-frame windows of neighbouring
-// markers are disjoint on average; EEGFX_DMA_NT=0/1 overrides.
-static bool wide_streaming(int64_t n_frames, int64_t n) {
-  static const int env = [] {
-    const char* e = getenv("EEGFX_DMA_NT");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
-  return env >= 0 ? env == 1 : (n > 0 && n_frames / n >= dev::kWin + 8);
 }
 
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
@@ -319,7 +322,7 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
   if (fmt == 0 && ct == 32 && !two) {  // configs[3]: the frame size as a compile-time constant
     // streaming (non-temporal) window reads and row stores when the windows are disjoint
-    if (wide_streaming(n_frames, n))
+    if (wide_streaming(n_frames, n, dev::kWin + 8))
       return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
                   : launch_wide_t<int16_t, false, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
     return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
