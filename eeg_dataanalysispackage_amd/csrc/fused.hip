@@ -59,9 +59,6 @@
 // packed fp32 op (116 VGPRs: 4 waves/SIMD); 1 = the same one sample per op (72 more VALU ops per
 // wave, 96 VGPRs: 5 waves/SIMD, 2 % faster than 0); 2 = packed pairs decoded just in time inside
 // level 1 (level1_lds: 94 VGPRs, 5 waves/SIMD, and the 72 VALU ops of 1 saved).
-#ifndef EEGFX_BASELINE_NT
-#define EEGFX_BASELINE_NT 0
-#endif
 #ifndef EEGFX_DECODE_SCALAR
 #define EEGFX_DECODE_SCALAR 2
 #endif
@@ -125,7 +122,7 @@ __device__ __forceinline__ u32x4_a4 load16_bulk(const uint8_t* __restrict__ raw,
   const bool full = want && A >= 0 && A + 16 <= nbytes;
   const u32x4_a16* src = (const u32x4_a16*)(full ? raw + A : safe_quad(raw, nbytes));
   u32x4_a4 v;
-  if constexpr (NT || EEGFX_BASELINE_NT) v = __builtin_nontemporal_load(src);
+  if constexpr (NT) v = __builtin_nontemporal_load(src);
   else v = *src;
   const u32x4_a4 z = {0u, 0u, 0u, 0u};
   return full ? v : z;
@@ -245,21 +242,9 @@ __device__ __forceinline__ void decode_lds(const int16_t* own, const int16_t* nx
 template <int CT, bool FAST>
 __device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nxt, float r, float b,
                                            double (&a1)[40]) {
-  const f32x2 rr = {r, r}, bb = {b, b};
-  double x[kIn];
-#pragma unroll
-  for (int i = 0; i < kIn / 2 - 4; ++i) {  // 32 outputs; output i reads x[2i .. 2i+9]
-#pragma unroll
-    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
-      const int16_t v0 = k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT];
-      const int16_t v1 = k + 1 < kSegLen ? own[(k + 1) * CT] : nxt[(k + 1 - kSegLen) * CT];
-      const f32x2 v = {(float)v0, (float)v1};
-      const f32x2 y = v * rr - bb;
-      x[k] = (double)y.x;
-      x[k + 1] = (double)y.y;
-    }
-    a1[i] = fir10<FAST, false>(x + 2 * i);
-  }
+  level1_jit<FAST>(
+      [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r, b,
+      a1);
 }
 
 // SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
