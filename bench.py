@@ -106,7 +106,7 @@ def valu_issue_from_profiles(applies):
     if not applies:
         return None
     try:
-        d = json.load(open(os.path.join(REPO, "profiles", "r01j_pmc_window_fma.json")))
+        d = json.load(open(os.path.join(REPO, "profiles", "r01k_pmc_window_fma.json")))
         return d["derived"]["valu_issue_utilisation"]
     except Exception:
         return None
@@ -294,7 +294,7 @@ def main():
                                        / FP64_VECTOR_PEAK_TFS, 4),
                          "valu_issue_utilisation": valu_issue_from_profiles(
                              C == 3 and args.numerics == "fma"),
-                         "source": "profiles/r01j_pmc_window_fma.json (fma, c3)"},
+                         "source": "profiles/r01k_pmc_window_fma.json (fma, c3)"},
             },
             "cpu_baseline": cpu,
         }
