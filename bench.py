@@ -40,8 +40,7 @@ FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (p
 FLOP_PER_SIGNAL = 2 * 5120                     # minimal a-path cascade, per channel
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
-WINDOW_KERNEL = {"exact": "window_kernel<int16,3>", "fma": "window_kernel<int16,3>",
-                 "mfma": "mfma_window_kernel<int16,3>"}
+WINDOW_KERNEL = "window_kernel<int16,3>"
 WORKLOADS = {
     "c3": {"ct": 3, "C": 3, "desc": "configs[1]: synthetic 1M epochs x 3 ch (Fz/Cz/Pz) multiplexed "
                                     "int16 @1000 Hz -> fe=dwt-8 48-dim L2-normalised features, per GPU"},
@@ -58,15 +57,18 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps; ~50 ms of sustained load brings the clocks to their steady (power-capped) state")
     ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
-    ap.add_argument("--workload", choices=["c3", "c32", "stream", "logreg", "svm"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c32", "stream", "dropin", "logreg", "svm"],
+                    default="c3",
                     help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "
                          "32-channel montage, every channel through the DWT, 512-dim); stream: "
                          "configs[4] (4 h recordings in pinned host memory, a marker every 100 ms, "
-                         "streamed to the device in chunks); logreg: the downstream classifier "
+                         "streamed to the device in chunks); dropin: configs[0]'s per-epoch "
+                         "IFeatureExtraction calls and the info.txt flow through the C ABI "
+                         "(latency, per calling thread); logreg: the downstream classifier "
                          "(MLlib LogisticRegressionWithSGD, 100 full-batch iterations) on the 1M "
                          "48-dim feature rows of c3; svm: the same with SVMWithSGD")
     ap.add_argument("--chunk-frames", type=int, default=1 << 23, help="stream workload chunk")
-    ap.add_argument("--numerics", choices=["exact", "fma", "mfma"], default="fma",
+    ap.add_argument("--numerics", choices=["exact", "fma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
     ap.add_argument("--alt-steps", type=int, default=10,
@@ -75,7 +77,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
-    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather leg")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather legs")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: 'gloo' runs the N>1 control flow without RCCL")
     ap.add_argument("--same-device", action="store_true",
@@ -136,6 +138,8 @@ def main():
 
     if args.workload == "stream":
         return bench_stream(args, rank, world, dev, dist if distributed else None)
+    if args.workload == "dropin":
+        return bench_dropin(args, rank, world, dev, dist if distributed else None)
     if args.workload in ("logreg", "svm"):
         return bench_logreg(args, rank, world, dev, dist if distributed else None)
     wl = WORKLOADS[args.workload]
@@ -220,19 +224,7 @@ def main():
 
     gather = None
     if distributed and not args.no_gather:
-        # RCCL over xGMI only moves the feature matrices: all-gather into rank order.
-        from eeg_dataanalysispackage_amd.sharding import gather_features
-        full = gather_features(out, world * n)  # warm
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        full = gather_features(out, world * n)
-        torch.cuda.synchronize(dev)
-        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
-        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        gather = {"op": "all_gather_into_tensor", "bytes_per_rank": n * 16 * C * 8,
-                  "ms": round(float(gt[0]) * 1e3, 3)}
-        del full
+        gather = bench_gather(args, ctx, out, n, C, rank, world, dev, dist)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -244,7 +236,7 @@ def main():
         achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9
         bpe = bytes_per_epoch(ct, C)
         path_gbs = n * bpe / (step_ms * 1e-3) / 1e9
-        kernels = (["baseline_kernel<int16,3>", WINDOW_KERNEL[args.numerics]] if C == 3 else
+        kernels = (["baseline_kernel<int16,3>", WINDOW_KERNEL] if C == 3 else
                    ["baseline_any_kernel<int16>", "window_wide_kernel<int16>"])
         prof = traffic_from_profiles(workload_key)
         line = {
@@ -302,11 +294,163 @@ def main():
             line["alt_numerics"] = alt
         if gather:
             line["gather"] = gather
+            if gather.get("ms") is not None:
+                # extract + gather: every rank ends holding the whole feature matrix
+                line["extract_plus_gather"] = {
+                    "value": round(world * n / ((elapsed / args.steps) + gather["ms"] * 1e-3), 1),
+                    "unit": "epochs/s", "gather_op": gather["op"]}
         print(json.dumps(line), flush=True)
 
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
+    """The only exchange of the path: assembling the [world*n][16C] feature matrix
+    in rank (= getData()) order on every rank.  Product leg: eegfx_gather through the C ABI (one
+    RCCL broadcast per rank inside a group, over xGMI), on a communicator created from an RCCL
+    unique id that rank 0 ships over the torch process group.  Comparison leg: torch's
+    all_gather_into_tensor (+ pad / concat for ragged shards).  Both are timed outside the
+    extraction steps (2 warm + 5 timed, max over ranks) and every rank checks its own rows."""
+    import torch
+    from eeg_dataanalysispackage_amd.sharding import Comm, gather_features
+
+    def timed(fn, reps=5):
+        fn()
+        fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = fn()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return res, float(t[0]) * 1e3
+
+    res = {"bytes_per_rank": n * 16 * C * 8, "rows": world * n}
+    if args.dist_backend == "nccl":
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(ctx, world, rank, uid[0])
+        full = torch.empty((world * n, 16 * C), dtype=torch.float64, device=dev)
+        full, ms = timed(lambda: comm.gather(out, world * n, out=full))
+        ok = bool(torch.equal(full[rank * n:(rank + 1) * n], out))
+        comm.close()
+        del full
+        res.update({"op": "eegfx_gather (RCCL broadcast per rank, grouped)", "ms": round(ms, 3),
+                    "rows_check": ok})
+    else:
+        res.update({"op": None, "ms": None, "note": "C-ABI gather needs RCCL (rehearsal backend)"})
+    full, ms_t = timed(lambda: gather_features(out, world * n))
+    res["torch_all_gather"] = {"ms": round(ms_t, 3),
+                               "rows_check": bool(torch.equal(full[rank * n:(rank + 1) * n], out))}
+    del full
+    if res["ms"] is None:
+        res["op"], res["ms"] = "torch all_gather_into_tensor", round(ms_t, 3)
+    return res
+
+
+def bench_dropin(args, rank, world, dev, dist):
+    """configs[0] through the C ABI, latency-bound: the reference calls
+    IFeatureExtraction.extractFeatures once per epoch (Spark map closures,
+    LogisticRegressionClassifier.java:55-61,90; serial loops, NeuralNetworkClassifier.java:78-86;
+    FeatureExtractionTest.java:62-67) and loads test-data/info.txt through OffLineDataProvider.
+    Reported per calling thread (one context per thread, as include/eegfx.h prescribes):
+      single_epoch  eegfx_extract_features_f64 on one host epoch (the JNI drop-in), median latency;
+      threads       the same call from T threads at once, each with its own context;
+      info_txt      OffLineDataProvider(info.txt).loadData() + features of its 11 epochs;
+    and beside them the C port (oracle, one thread) on the same epoch."""
+    import threading
+    import torch
+    import eeg_dataanalysispackage_amd as fx
+    from oracle import oracle
+    data = os.path.join(REPO, "tests", "golden", "test-data")
+    base = os.path.join(data, "DoD", "DoD2015_01")
+    raw = fx.read_raw(base + ".vhdr", base + ".eeg")
+    pos, _, _ = fx.plan_markers(fx.read_markers(base + ".vmrk"), raw.shape[0], 1)
+    ep = oracle.decode_epochs(raw, [0, 1, 2], [0.1] * 3, pos)
+    reps = max(200, args.steps * 10)
+
+    def lat(fn, k=reps):
+        for _ in range(20):
+            fn()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), float(np.percentile(ts, 99))
+
+    ctx = fx.Context(dev.index, numerics=args.numerics)
+    one = np.ascontiguousarray(ep[:1])
+    outb = np.empty((1, 48))
+    med, p99 = lat(lambda: ctx.extract_features(one, out=outb))
+    want = oracle.extract_features(one)
+    parity = bool(np.array_equal(outb, want) if args.numerics == "exact"
+                  else np.max(np.abs(outb - want)) <= 1e-9)
+    fe = fx.WaveletTransform(context=ctx)
+    med_fe, _ = lat(lambda: fe.extractFeatures(ep[0]))
+    # T threads, one context each, calling concurrently (Spark local[T])
+    threads = {}
+    for T in (2, 4, 8):
+        ctxs = [fx.Context(dev.index, numerics=args.numerics) for _ in range(T)]
+        per = [0.0] * T
+        k = reps // 2
+
+        def work(i):
+            o = np.empty((1, 48))
+            for _ in range(10):
+                ctxs[i].extract_features(one, out=o)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                ctxs[i].extract_features(one, out=o)
+            per[i] = (time.perf_counter() - t0) / k
+        th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for c in ctxs:
+            c.close()
+        threads[str(T)] = {"per_thread_epochs_per_s": round(1.0 / float(np.mean(per)), 1),
+                           "aggregate_epochs_per_s": round(sum(1.0 / p for p in per), 1)}
+    # info.txt end to end (configs[0]'s data) through the C-ABI provider
+    info = os.path.join(data, "infoTrain.txt")
+
+    def info_flow():
+        odp = fx.OffLineDataProvider([info], context=ctx)
+        odp.loadData()
+        f = odp.getFeatures()
+        odp.close()
+        return f
+    med_info, _ = lat(info_flow, k=max(20, args.steps))
+    f_info = info_flow()
+    # the C port on the same epoch, one thread (the per-thread rate of the CPU baseline)
+    med_cpu, _ = lat(lambda: oracle.extract_features(one, faithful=True), k=reps)
+    ctx.close()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "per-call IFeatureExtraction latency through the C ABI (configs[0] drop-in)",
+            "value": round(1.0 / med, 1), "unit": "epochs/s per calling thread",
+            "n_gpus": world, "steps": reps, "warmup": 20, "ms_per_step": round(med * 1e3, 4),
+            "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "f64",
+            "data": "reference test-data (DoD2015_01, infoTrain.txt)",
+            "config": {"workload": "configs[0]: one host epoch per eegfx_extract_features_f64 "
+                                   "call (zero-copy pinned staging), numerics " + args.numerics,
+                       "parity": parity},
+            "single_epoch": {"median_us": round(med * 1e6, 2), "p99_us": round(p99 * 1e6, 2),
+                             "python_WaveletTransform_median_us": round(med_fe * 1e6, 2)},
+            "threads": threads,
+            "info_txt": {"epochs": int(f_info.shape[0]), "median_ms": round(med_info * 1e3, 3),
+                         "epochs_per_s": round(f_info.shape[0] / med_info, 1),
+                         "feature_sum": oracle.java_feature_sum(f_info)},
+            "cpu_baseline": {"value": round(1.0 / med_cpu, 1), "unit": "epochs/s per thread",
+                             "cores": 1, "kind": "port",
+                             "sample": "the same epoch, oracle C restatement (full pyramid), "
+                                       f"median of {reps} calls"},
+        }), flush=True)
 
 
 def bench_stream(args, rank, world, dev, dist):

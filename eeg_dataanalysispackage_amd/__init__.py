@@ -10,12 +10,12 @@ Host mirror of the reference's hot-path API over the libeegfx C ABI (include/eeg
 from ._lib import EegfxError, LIB_PATH, lib
 from .brainvision import (ChannelInfo, EEGMarker, Header, plan_markers, read_header,
                           read_markers, read_raw, recording_frames)
-from .context import Context, device_count, dwt8_operator
+from .context import Context, device_count
 from .data_provider import OffLineDataProvider
 from .feature_extraction import IFeatureExtraction, WaveletTransform
 
 __all__ = [
     "Context", "ChannelInfo", "EEGMarker", "EegfxError", "Header", "IFeatureExtraction",
-    "LIB_PATH", "OffLineDataProvider", "WaveletTransform", "device_count", "dwt8_operator", "lib",
+    "LIB_PATH", "OffLineDataProvider", "WaveletTransform", "device_count", "lib",
     "plan_markers", "read_header", "read_markers", "read_raw", "recording_frames",
 ]

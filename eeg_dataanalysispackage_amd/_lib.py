@@ -30,7 +30,6 @@ MEM_HOST = 0
 MEM_DEVICE = 1
 EXACT = 0
 FMA = 1
-MFMA = 2
 PRESTIMULUS = 100
 POSTSTIMULUS = 750
 
@@ -73,6 +72,7 @@ SIGNATURES = {
     "eegfx_device_count": (c_int, [POINTER(c_int)]),
     "eegfx_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
     "eegfx_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "eegfx_ctx_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
     "eegfx_ctx_set_numerics": (c_int, [c_void_p, c_int]),
     "eegfx_ctx_synchronize": (c_int, [c_void_p]),
     "eegfx_ctx_kernel_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double),
@@ -92,7 +92,6 @@ SIGNATURES = {
     "eegfx_process_recording": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p,
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
-    "eegfx_dwt8_operator": (c_int, [c_void_p]),
     "eegfx_logreg_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                        c_double, c_double, c_double, c_double, c_void_p,
                                        POINTER(c_int32), c_int]),
@@ -107,6 +106,7 @@ SIGNATURES = {
                                           POINTER(c_int64), c_void_p, c_void_p, POINTER(c_int64),
                                           c_int]),
     "eegfx_shard_range": (c_int, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
+    "eegfx_gather_schedule": (c_int, [c_int64, c_int32, c_void_p, c_void_p]),
     "eegfx_comm_unique_id": (c_int, [c_void_p]),
     "eegfx_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_void_p, POINTER(c_void_p)]),
     "eegfx_comm_init_all": (c_int, [POINTER(c_void_p), c_int32, POINTER(c_void_p)]),

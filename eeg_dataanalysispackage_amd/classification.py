@@ -20,7 +20,7 @@ from typing import Dict, Optional, Sequence
 import numpy as np
 
 from ._lib import EegfxError, check, lib, ptr
-from .context import Context, _is_device, _mem
+from .context import Context, _contig, _is_device, _mem
 
 # LogisticRegressionWithSGD() defaults (MLlib 1.6.2) and GradientDescent's convergence tolerance
 DEFAULT_STEP_SIZE = 1.0
@@ -34,10 +34,11 @@ def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini
            convergence_tol, initial_weights):
     if _is_device(X) != _is_device(y):
         raise ValueError("X and y must both be host or both be device arrays")
-    if not _is_device(X):
-        X = np.ascontiguousarray(X, dtype=np.float64)
-        y = np.ascontiguousarray(y, dtype=np.float64)
+    X = _contig(X, np.float64)
+    y = _contig(y, np.float64)
     n, d = int(X.shape[0]), int(X.shape[1])
+    if X.ndim != 2 or y.ndim != 1 or int(y.shape[0]) != n:
+        raise ValueError(f"X must be [n][d] and y [n], got {tuple(X.shape)} and {tuple(y.shape)}")
     w = (np.zeros(d) if initial_weights is None
          else np.array(initial_weights, dtype=np.float64).copy())
     it = c_int32()
@@ -49,12 +50,12 @@ def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini
 
 def _predict(entry, ctx: Context, X, weights, intercept, threshold):
     w = np.ascontiguousarray(weights, dtype=np.float64)
+    X = _contig(X, np.float64)
     n, d = int(X.shape[0]), int(X.shape[1])
     if _is_device(X):
         import torch
         out = torch.empty(n, dtype=torch.float64, device=X.device)
     else:
-        X = np.ascontiguousarray(X, dtype=np.float64)
         out = np.empty(n, dtype=np.float64)
     t = math.nan if threshold is None else float(threshold)
     check(getattr(lib(), entry)(ctx.handle, ptr(X), n, d, ptr(w), float(intercept), t, ptr(out),
@@ -126,16 +127,19 @@ class ClassificationStatistics:
 def reference_statistics(predictions, labels) -> ClassificationStatistics:
     """LogisticRegressionClassifier.test :129-137: MulticlassMetrics' confusion matrix (rows =
     actual, columns = predicted, labels ascending) flattened column-major by toArray and read as
-    tn, fp, fn, tp = cm[0], cm[1], cm[2], cm[3].  With a single class present the matrix is 1x1
+    tn, fp, fn, tp = cm[0], cm[1], cm[2], cm[3].  Spark 1.6's ``labels`` are the classes of the
+    ACTUAL labels only (``tpByClass.keys``, built from ``labelCountByClass``), and a prediction
+    of a class outside them falls out of the matrix.  With a single actual class the matrix is 1x1
     and the reference's cm[1] throws; so does this (IndexError)."""
     p = np.asarray(predictions, dtype=np.float64)
     a = np.asarray(labels, dtype=np.float64)
-    classes = sorted(set(a.tolist()) | set(p.tolist()))
+    classes = sorted(set(a.tolist()))
     k = len(classes)
     cm = np.zeros((k, k), dtype=np.int64)
     idx = {c: i for i, c in enumerate(classes)}
     for ai, pi in zip(a.tolist(), p.tolist()):
-        cm[idx[ai], idx[pi]] += 1
+        if pi in idx:
+            cm[idx[ai], idx[pi]] += 1
     flat = cm.flatten(order="F")
     tn, fp, fn, tp = (int(flat[0]), int(flat[1]), int(flat[2]), int(flat[3]))
     return ClassificationStatistics(tp, tn, fp, fn)

@@ -2,7 +2,12 @@
 
 Arrays may be numpy arrays (host memory: the library stages them through HBM and returns after
 the results are copied back) or torch tensors on a ROCm device (device memory: the work is
-enqueued on the context stream and the call returns without synchronising).
+enqueued on the context stream and the call returns without synchronising).  Device calls are
+ordered with torch's current stream on both sides: the context stream waits for the work that
+produced the inputs, and torch's stream waits for the kernels before anything later uses (or
+frees) the buffers.  Marker positions held in device memory are validated by the kernels; a
+violation raises ``IndexError`` (the reference's ArrayIndexOutOfBoundsException) from the next
+``Context.synchronize()``.
 """
 from __future__ import annotations
 
@@ -27,19 +32,40 @@ def _mem(*arrays) -> int:
     return _lib.MEM_DEVICE if kinds.pop() else _lib.MEM_HOST
 
 
+_TORCH_NAMES = {np.dtype(np.float64): "float64", np.dtype(np.int64): "int64",
+                np.dtype(np.int32): "int32", np.dtype(np.float32): "float32",
+                np.dtype(np.int16): "int16"}
+
+
 def _contig(a, dtype):
+    """Host arrays are converted to `dtype`; device tensors are passed as they are, so they must
+    already have it (the kernels read the raw bytes: an int32 position tensor read as int64 would
+    address past its allocation)."""
     if _is_device(a):
+        want = _TORCH_NAMES[np.dtype(dtype)]
+        if str(a.dtype) != "torch." + want:
+            raise ValueError(f"device tensor has dtype {a.dtype}, expected torch.{want}")
         if not a.is_contiguous():
             raise ValueError("device tensors must be contiguous")
         return a
     return np.ascontiguousarray(a, dtype=dtype)
 
 
+def _check_out(out, shape, dtype="float64"):
+    """A caller-supplied output: right shape, dtype and contiguity (the kernels write it raw)."""
+    if tuple(out.shape) != tuple(shape):
+        raise ValueError(f"out has shape {tuple(out.shape)}, expected {tuple(shape)}")
+    if _is_device(out):
+        if str(out.dtype) != "torch." + dtype or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous torch.{dtype} tensor")
+    elif out.dtype != np.dtype(dtype) or not out.flags["C_CONTIGUOUS"]:
+        raise ValueError(f"out must be a C-contiguous {dtype} array")
+    return out
+
+
 class Context:
     """One HIP device + stream (eegfx_ctx).  numerics: "exact" (bit-exact to the reference
-    order of operations, default), "fma" (fused multiply-add filter bank, <= 1e-9 relative) or
-    "mfma" (the window as one 16x512 fp64 operator on the matrix cores, <= 1e-9 relative; layouts
-    without a matrix kernel run the "fma" filter bank)."""
+    order of operations, default) or "fma" (fused multiply-add filter bank, <= 1e-9 relative)."""
 
     def __init__(self, device: int = 0, numerics: str = "exact"):
         h = c_void_p()
@@ -56,18 +82,58 @@ class Context:
         return self._h
 
     def set_numerics(self, numerics: str) -> None:
-        mode = {"exact": _lib.EXACT, "fma": _lib.FMA, "mfma": _lib.MFMA}[numerics]
+        modes = {"exact": _lib.EXACT, "fma": _lib.FMA}
+        if numerics not in modes:
+            raise ValueError(f"numerics must be one of {sorted(modes)}, got {numerics!r}")
+        mode = modes[numerics]
         check(lib().eegfx_ctx_set_numerics(self.handle, mode))
         self.numerics = numerics
 
     def set_stream(self, stream_handle: Optional[int]) -> None:
         check(lib().eegfx_ctx_set_stream(self.handle, c_void_p(stream_handle or 0)))
 
+    def stream_handle(self) -> int:
+        """The hipStream_t the context enqueues on."""
+        h = c_void_p()
+        check(lib().eegfx_ctx_stream(self.handle, ctypes.byref(h)))
+        return int(h.value or 0)
+
+    def _enter_device(self, ref):
+        """Orders the context stream after torch's current stream (the producers of the inputs);
+        returns the pair for _leave_device, or None when they are the same stream."""
+        import torch
+        cur = torch.cuda.current_stream(ref.device)
+        mine = self.stream_handle()
+        if cur.cuda_stream == mine:
+            return None
+        ext = torch.cuda.ExternalStream(mine, device=ref.device)
+        ext.wait_stream(cur)
+        return cur, ext
+
+    @staticmethod
+    def _leave_device(pair) -> None:
+        """Orders torch's current stream after the kernels just enqueued."""
+        if pair is not None:
+            cur, ext = pair
+            cur.wait_stream(ext)
+
+    def _call(self, mem, ref, fn, *args):
+        pair = self._enter_device(ref) if mem == _lib.MEM_DEVICE else None
+        try:
+            check(fn(*args))
+        finally:
+            self._leave_device(pair)
+
     def set_timing(self, enable: bool) -> None:
         check(lib().eegfx_ctx_set_timing(self.handle, 1 if enable else 0))
 
     def synchronize(self) -> None:
-        check(lib().eegfx_ctx_synchronize(self.handle))
+        """Waits for the context stream.  Raises IndexError when a kernel met a device-resident
+        marker position the reference would not cut (OffLineDataProvider.java:220-225)."""
+        rc = lib().eegfx_ctx_synchronize(self.handle)
+        if rc == _lib.EEGFX_ERANGE:
+            raise IndexError(lib().eegfx_last_error().decode(errors="replace"))
+        check(rc)
 
     def kernel_stats(self):
         """(timed launches, summed duration in ms, algorithmic bytes) of the dominant kernel
@@ -101,6 +167,7 @@ class Context:
         """Raw multiplexed recording (int16 or float32, n_frames x n_channels_total) ->
         baseline-corrected epochs double[n][C][750] (OffLineDataProvider.java:216-233)."""
         cols_a, res_a = self._sel(cols, res)
+        raw = _raw(raw)
         fmt = _fmt(raw)
         n_frames = _numel(raw) // n_channels_total
         pos = _contig(pos, np.int64)
@@ -108,9 +175,10 @@ class Context:
         C = len(cols_a)
         if out is None:
             out = _empty_like_mem(raw, (n, C, _lib.POSTSTIMULUS), "float64")
+        _check_out(out, (n, C, _lib.POSTSTIMULUS))
         mem = _mem(raw, pos, out)
-        check(lib().eegfx_cut_epochs_f64(self.handle, ptr(raw), fmt, n_frames, n_channels_total,
-                                         ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out), mem))
+        self._call(mem, raw, lib().eegfx_cut_epochs_f64, self.handle, ptr(raw), fmt, n_frames,
+                   n_channels_total, ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out), mem)
         return out
 
     def extract_features(self, epochs, name=8, epoch_size=512, skip=175, feature_size=16,
@@ -123,14 +191,16 @@ class Context:
         n, C = shape[0], shape[1]
         if out is None:
             out = _empty_like_mem(epochs, (n, C * feature_size), "float64")
+        _check_out(out, (n, C * feature_size))
         mem = _mem(epochs, out)
-        check(lib().eegfx_extract_features_f64(self.handle, ptr(epochs), n, C, name, epoch_size,
-                                               skip, feature_size, ptr(out), mem))
+        self._call(mem, epochs, lib().eegfx_extract_features_f64, self.handle, ptr(epochs), n, C,
+                   name, epoch_size, skip, feature_size, ptr(out), mem)
         return out
 
     def process_recording(self, raw, n_channels_total: int, cols, res, pos, out=None):
         """Fused hot path: raw recording + marker positions -> dwt-8 features [n][16*C]."""
         cols_a, res_a = self._sel(cols, res)
+        raw = _raw(raw)
         fmt = _fmt(raw)
         n_frames = _numel(raw) // n_channels_total
         pos = _contig(pos, np.int64)
@@ -138,10 +208,10 @@ class Context:
         C = len(cols_a)
         if out is None:
             out = _empty_like_mem(raw, (n, 16 * C), "float64")
+        _check_out(out, (n, 16 * C))
         mem = _mem(raw, pos, out)
-        check(lib().eegfx_process_recording(self.handle, ptr(raw), fmt, n_frames,
-                                            n_channels_total, ptr(cols_a), ptr(res_a), C,
-                                            ptr(pos), n, ptr(out), mem))
+        self._call(mem, raw, lib().eegfx_process_recording, self.handle, ptr(raw), fmt, n_frames,
+                   n_channels_total, ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out), mem)
         return out
 
     def plan_markers(self, positions, stimulus_index, n_frames: int, guessed: int,
@@ -152,6 +222,8 @@ class Context:
         from ctypes import byref
         if _is_device(positions):
             import torch
+            positions = _contig(positions, np.int64)
+            stimulus_index = _contig(stimulus_index, np.int32)
             n = int(positions.numel())
             pos_out = torch.empty(max(1, n), dtype=torch.int64, device=positions.device)
             lab_out = torch.empty(max(1, n), dtype=torch.float64, device=positions.device)
@@ -163,10 +235,10 @@ class Context:
             lab_out = np.empty(max(1, n), dtype=np.float64)
         bal = c_int64(balance)
         k = c_int64()
-        check(lib().eegfx_plan_markers_device(self.handle, ptr(positions), ptr(stimulus_index), n,
-                                              int(n_frames), int(guessed), byref(bal),
-                                              ptr(pos_out), ptr(lab_out), byref(k),
-                                              _mem(positions, stimulus_index, pos_out)))
+        mem = _mem(positions, stimulus_index, pos_out)
+        self._call(mem, positions, lib().eegfx_plan_markers_device, self.handle, ptr(positions),
+                   ptr(stimulus_index), n, int(n_frames), int(guessed), byref(bal), ptr(pos_out),
+                   ptr(lab_out), byref(k), mem)
         return pos_out[:k.value], lab_out[:k.value], bal.value
 
     def process_recording_streamed(self, raw, n_channels_total: int, cols, res, pos,
@@ -184,6 +256,7 @@ class Context:
         C = len(cols_a)
         if out is None:
             out = np.empty((n, 16 * C), dtype=np.float64)
+        _check_out(out, (n, 16 * C))
         check(lib().eegfx_process_recording_streamed(
             self.handle, ptr(raw), fmt, n_frames, n_channels_total, ptr(cols_a), ptr(res_a), C,
             ptr(pos), n, ptr(out), int(chunk_frames)))
@@ -193,18 +266,10 @@ class Context:
         """Fills a device int16 tensor (n_frames x n_channels) with the synthetic recording."""
         if not _is_device(dst):
             raise ValueError("synth_recording writes a device tensor")
+        dst = _contig(dst, np.int16)
         n_frames = dst.numel() // n_channels
-        check(lib().eegfx_synth_recording(self.handle, ptr(dst), n_frames, n_channels,
-                                          ctypes.c_uint64(seed)))
-
-
-def dwt8_operator() -> np.ndarray:
-    """The fe=dwt-8 window transform as a 16 x 512 matrix (host; eegfx_dwt8_operator):
-    row r of the first 16 coefficients (a6 ++ d6, before normalisation) of a window x is
-    ``M[r] @ x`` -- the operator the "mfma" numerics applies on the FP64 matrix cores."""
-    m = np.empty((16, 512), dtype=np.float64)
-    check(lib().eegfx_dwt8_operator(ptr(m)))
-    return m
+        self._call(_lib.MEM_DEVICE, dst, lib().eegfx_synth_recording, self.handle, ptr(dst),
+                   n_frames, n_channels, ctypes.c_uint64(seed))
 
 
 def device_count() -> int:
@@ -215,6 +280,16 @@ def device_count() -> int:
 
 def _numel(a) -> int:
     return int(a.numel()) if hasattr(a, "numel") and callable(a.numel) else int(np.asarray(a).size)
+
+
+def _raw(raw):
+    """The recording: a contiguous int16 / float32 array (host) or tensor (device)."""
+    _fmt(raw)
+    if _is_device(raw):
+        if not raw.is_contiguous():
+            raise ValueError("device tensors must be contiguous")
+        return raw
+    return np.ascontiguousarray(raw)
 
 
 def _fmt(raw) -> int:

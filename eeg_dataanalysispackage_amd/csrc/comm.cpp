@@ -48,6 +48,19 @@ int eegfx_shard_range(int64_t n, int32_t rank, int32_t world, int64_t* start, in
   });
 }
 
+int eegfx_gather_schedule(int64_t n_total, int32_t world, int64_t* offsets, int64_t* counts) {
+  return guarded([&] {
+    if (n_total < 0 || world < 1 || !offsets || !counts)
+      fail(EEGFX_EINVAL, "gather_schedule(n=%lld, world=%d)", (long long)n_total, world);
+    for (int r = 0; r < world; ++r) {
+      int64_t s = 0, e = 0;
+      shard(n_total, world, r, &s, &e);
+      offsets[r] = s;
+      counts[r] = e - s;
+    }
+  });
+}
+
 int eegfx_comm_unique_id(void* id) {
   return guarded([&] {
     if (!id) fail(EEGFX_EINVAL, "null id buffer");
@@ -115,20 +128,20 @@ int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t
                  double* out) {
   return guarded([&] {
     if (!comm || !out || n_total < 0 || cols < 1) fail(EEGFX_EINVAL, "gather arguments");
-    int64_t s = 0, e = 0;
-    shard(n_total, comm->world, comm->rank, &s, &e);
-    if (e > s && !local) fail(EEGFX_EINVAL, "null local rows");
+    std::vector<int64_t> off((size_t)comm->world), cnt((size_t)comm->world);
+    const int rc = eegfx_gather_schedule(n_total, comm->world, off.data(), cnt.data());
+    if (rc != EEGFX_OK) fail(rc, "%s", last_error().c_str());
+    if (cnt[(size_t)comm->rank] > 0 && !local) fail(EEGFX_EINVAL, "null local rows");
     if (hipSetDevice(ctx_device(comm->ctx)) != hipSuccess)
       fail(EEGFX_EHIP, "hipSetDevice(%d)", ctx_device(comm->ctx));
     const hipStream_t st = (hipStream_t)ctx_stream(comm->ctx);
     nccl_check(ncclGroupStart(), "ncclGroupStart");
     ncclResult_t r = ncclSuccess;
     for (int root = 0; root < comm->world && r == ncclSuccess; ++root) {
-      int64_t rs = 0, re = 0;
-      shard(n_total, comm->world, root, &rs, &re);
-      if (re == rs) continue;  // same decision on every rank
-      r = ncclBroadcast(root == comm->rank ? (const void*)local : nullptr, out + rs * cols,
-                        (size_t)((re - rs) * cols), ncclDouble, root, comm->comm, st);
+      if (cnt[(size_t)root] == 0) continue;  // same decision on every rank
+      r = ncclBroadcast(root == comm->rank ? (const void*)local : nullptr,
+                        out + off[(size_t)root] * cols, (size_t)(cnt[(size_t)root] * cols),
+                        ncclDouble, root, comm->comm, st);
     }
     const ncclResult_t g = ncclGroupEnd();
     nccl_check(r, "ncclBroadcast");

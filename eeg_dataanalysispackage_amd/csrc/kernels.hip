@@ -26,10 +26,17 @@ template <typename T>
 __global__ __launch_bounds__(256) void cut_epochs_kernel(const T* __restrict__ raw, int64_t n_frames,
                                                          int ct, ChanSel sel, int C,
                                                          const int64_t* __restrict__ pos,
-                                                         double* __restrict__ out) {
+                                                         double* __restrict__ out,
+                                                         int* __restrict__ err) {
   __shared__ float base[kMaxChannels];
   const int64_t e = blockIdx.x;
-  const int64_t p = pos[e];
+  const int64_t p0 = pos[e];
+  // OffLineDataProvider.java:220-225 (see fused.hip position_ok): an invalid position is flagged
+  // and cut as pos = 100
+  const bool ok = p0 >= kPre && p0 - kPre <= n_frames;
+  if (threadIdx.x == 0 && !ok && err)
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int64_t p = ok ? p0 : kPre;
   const int64_t lo = p - kPre;
   if ((int)threadIdx.x < C) {
     const int c = threadIdx.x;
@@ -64,7 +71,8 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
                                                         const float* __restrict__ base,
                                                         double* __restrict__ out) {
   const int64_t e = blockIdx.x;
-  const int64_t p = pos[e];
+  const int64_t p0 = pos[e];
+  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : kPre;  // flagged by the baselines
   double* o = out + e * C * kPost;
   for (int idx = 2 * (int)threadIdx.x; idx < C * kPost; idx += 2 * (int)blockDim.x) {
     const int c = idx / kPost;
@@ -72,8 +80,8 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
     const int col = sel.col[c];
     const float r = sel.res[c], b = base[e * C + c];
     // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
-    const float v0 = f < n_frames ? (float)raw[f * ct + col] * r : 0.0f;
-    const float v1 = f + 1 < n_frames ? (float)raw[(f + 1) * ct + col] * r : 0.0f;
+    const float v0 = f >= 0 && f < n_frames ? (float)raw[f * ct + col] * r : 0.0f;
+    const float v1 = f + 1 >= 0 && f + 1 < n_frames ? (float)raw[(f + 1) * ct + col] * r : 0.0f;
     *(double2*)(o + idx) = make_double2((double)(v0 - b), (double)(v1 - b));
   }
 }
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(256) void synth_kernel(int16_t* __restrict__ dst, i
 // ---- launchers ---------------------------------------------------------------------------------
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                             double* out, void* scratch) {
+                             double* out, void* scratch, int* err) {
   if (n == 0) return hipSuccess;
   dim3 grid((unsigned)n), block(256);
   // baselines by the staged kernels when a layout fits them, then the coalesced write pass
@@ -174,9 +182,9 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
   const bool aligned = ((uintptr_t)out & 15) == 0;  // the write pass stores 16-byte pairs
   if (!aligned) scratch = nullptr;
   if (scratch && fmt == 0 && ct == 3 && C == 3)
-    be = launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch);
+    be = launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch, err);
   else if (scratch && baseline_any_supported(fmt, ct, C))
-    be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch);
+    be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err);
   if (be == hipSuccess) {
     if (fmt == 0)
       hipLaunchKernelGGL(dev::cut_write_kernel<int16_t>, grid, block, 0, st, (const int16_t*)raw,
@@ -188,10 +196,10 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
   }
   if (fmt == 0)
     hipLaunchKernelGGL(dev::cut_epochs_kernel<int16_t>, grid, block, 0, st,
-                       (const int16_t*)raw, n_frames, ct, sel, C, pos, out);
+                       (const int16_t*)raw, n_frames, ct, sel, C, pos, out, err);
   else
     hipLaunchKernelGGL(dev::cut_epochs_kernel<float>, grid, block, 0, st, (const float*)raw,
-                       n_frames, ct, sel, C, pos, out);
+                       n_frames, ct, sel, C, pos, out, err);
   return hipGetLastError();
 }
 

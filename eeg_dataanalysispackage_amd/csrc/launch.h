@@ -16,34 +16,37 @@ struct ChanSel {
   float res[kMaxChannels];
 };
 
+// err: device-visible int (the context's host-mapped error word) set to 1 when a kernel reads a
+// marker position the reference would not cut (pos - 100 outside [0, n_frames]); may be null.
 // scratch: fused_scratch_bytes(n, C) bytes for the baselines (nullptr: single-kernel fallback)
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                             double* out, void* scratch);
+                             double* out, void* scratch, int* err);
 // row_stride: doubles between consecutive (epoch, channel) rows of `ep` (750 for materialised
 // epochs, 512 for the window-only rows the host path stages)
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
                                        int nfeat, bool fast, double* out, int row_stride = 750);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
+// Non-temporal reads pay when the regions neighbouring epochs read do not overlap: the average
+// marker spacing n_frames / n is at least min_spacing frames (fused.hip).
+bool streaming_reads(int64_t n_frames, int64_t n, int64_t min_spacing);
+
 // Fused raw -> features (fused.hip): baseline_kernel then window_kernel.  `scratch` holds
 // fused_scratch_bytes(n, C) bytes of device memory (the per-epoch baselines).  fused_supported
-// says whether a fused kernel covers (fmt, ct, C); otherwise the caller runs cut + features
-// through a device scratch buffer.
+// says whether the 3-channel kernels cover (fmt, ct, C); the any-layout kernels of wide.hip take
+// the rest.
 bool fused_supported(int fmt, int ct, int C, const double* out);
 size_t fused_scratch_bytes(int64_t n, int C);
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 void* scratch);
+                                 void* scratch, int* err);
 hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
                                const void* scratch, double* out);
 // Algorithmic HBM bytes per epoch of window_kernel (the dominant kernel): window frames, the
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);
-// True when window_kernel folds the baselines itself (then launch_fused_baseline is skipped and
-// launch_fused_window ignores `scratch`).
-bool fused_baseline_in_window();
 
 // Any-layout fused path (wide.hip): baseline_any_kernel then window_wide_kernel, same scratch
 // contract as the 3-channel kernels.  wide_supported: int16/float32, C <= 64, one epoch's staged
@@ -52,22 +55,10 @@ bool wide_supported(int fmt, int ct, int C);
 bool baseline_any_supported(int fmt, int ct, int C);
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch);
+                               void* scratch, int* err);
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
                               const void* scratch, double* out);
-
-// Collapsed-operator window on the FP64 matrix cores (mfma.hip), the EEGFX_MFMA numerics: same
-// baseline scratch as the fused path; mrows = dwt8_operator_rows() on the device (8 KB).
-bool mfma_supported(int fmt, int ct, int C);
-hipError_t launch_mfma_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
-                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                              const void* scratch, const double* mrows, double* out);
-// dwt8_operator.cpp: M[16][512] with coefficient r = sum_k M[r][k] x[k] (a6 ++ d6); M is
-// block-circulant, rows[0][.] = M[0][.] (a6[0]) and rows[1][.] = M[8][.] (d6[0]) define it.
-void dwt8_operator(double* M);
-void dwt8_operator_rows(double* rows);
-constexpr int kOperatorRowDoubles = 2 * 512;
 
 // logreg.hip: MLlib LogisticRegressionWithSGD (full batch) on device.  State block: iteration
 // count, flag (0 running, 1 converged / done, 2 invalid labels), then the d weights.

@@ -289,10 +289,7 @@ hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrStat
 }
 
 int lr_grid(int64_t n) {
-  static const int64_t cap = [] {
-    const char* e = getenv("EEGFX_LR_G");
-    return (int64_t)(e ? atoi(e) : 512);
-  }();
+  constexpr int64_t cap = 512;  // 2 workgroups per CU
   const int64_t g = (n + 16 * dev::kLrWaves - 1) / (16 * dev::kLrWaves);  // >= 16 rows per wave
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }

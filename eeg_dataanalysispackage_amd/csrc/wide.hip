@@ -18,7 +18,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 
 #include "dwt8.h"
 #include "launch.h"
@@ -40,7 +39,8 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
                                                            int64_t n_frames, int ct, ChanSel sel,
                                                            int C, const int64_t* __restrict__ pos,
                                                            int64_t n, int EB, int BSTQ,
-                                                           float* __restrict__ bout) {
+                                                           float* __restrict__ bout,
+                                                           int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t sB[256];
   const int FB = ct * (int)sizeof(T);
@@ -51,7 +51,13 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
   const int nw = blockDim.x / 64;
   const int NQ = BSTQ - 1;  // quads staged per epoch
   const int rows = (NQ + 63) / 64;
-  if (tid < ne) sB[tid] = (pos[e0 + tid] - kPre) * FB;
+  if (tid < ne) {
+    const int64_t p = pos[e0 + tid];
+    // OffLineDataProvider.java:220-225 (see fused.hip position_ok)
+    const bool ok = p >= kPre && p - kPre <= n_frames;
+    if (!ok && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sB[tid] = ((ok ? p : kPre) - kPre) * FB;  // an invalid position is cut as pos = 100
+  }
   __syncthreads();
   int m = 0, j = w;
   while (j >= rows) { j -= rows; ++m; }
@@ -102,12 +108,12 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
   bout[(e0 + me) * C + c] = b / (float)kPre;
 }
 
-// One 16-byte quad of the recording at byte offset A (16-aligned), zero past the end.
+// One 16-byte quad of the recording at byte offset A (16-aligned), zero outside it.
 __device__ __forceinline__ wq_a4 wide_load16(const uint8_t* __restrict__ raw, int64_t nbytes,
                                              int64_t A) {
-  if (A + 16 <= nbytes) return *(const wq_a16*)(raw + A);
+  if (A >= 0 && A + 16 <= nbytes) return *(const wq_a16*)(raw + A);
   wq_a4 v = {0u, 0u, 0u, 0u};
-  if (A < nbytes) {
+  if (A >= 0 && A < nbytes) {
     uint32_t t[4] = {0u, 0u, 0u, 0u};
     for (int i = 0; i < 4; ++i) {
       const int64_t a = A + 4 * i;
@@ -153,23 +159,28 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   const int nw = blockDim.x / 64;
   const int nrows = (EQ + 63) / 64;
   const float inv_segq = 1.0f / (float)SEGQ;
+  // invalid positions (flagged by baseline_any_kernel) are cut as pos = 100, before any offset
+  // is formed from them
+  auto wpos = [&](int m) {
+    const int64_t p = pos[e0 + m];
+    return p >= kPre && p - kPre <= n_frames ? p : (int64_t)kPre;
+  };
   int64_t Bq[EPW];
 #pragma unroll
-  for (int m = 0; m < EPW; ++m)
-    Bq[m] = (((pos[e0 + (m < ne ? m : 0)] + 175) * FB) & ~(int64_t)15);
+  for (int m = 0; m < EPW; ++m) Bq[m] = (((wpos(m < ne ? m : 0) + 175) * FB) & ~(int64_t)15);
   const int64_t span = (int64_t)64 * FB * 7 + 16 * SEGQ;
 #pragma unroll
   for (int m = 0; m < EPW; ++m) {
     if (m >= ne) break;  // uniform
     const uint8_t* sb = raw + Bq[m];
-    const bool full = Bq[m] + span <= nbytes;
+    const bool full = Bq[m] >= 0 && Bq[m] + span <= nbytes;
     for (int j = w; j < nrows; j += nw) {
       const int i = 64 * j + lane;
       const int sg = (int)(((float)i + 0.5f) * inv_segq);
       const uint32_t off = (uint32_t)(64 * FB * sg + 16 * (i - sg * SEGQ));
       uint8_t* dst = win + ((size_t)m * EQ + 64 * j) * 16;
       if (i < EQ) {
-        if (full || Bq[m] + off + 16 <= nbytes) {
+        if (full || (Bq[m] + off >= 0 && Bq[m] + off + 16 <= nbytes)) {
           dma16_s<STREAM>(sb, off, dst);
         } else {
           const wq_a4 v = wide_load16(raw, nbytes, Bq[m] + off);
@@ -189,7 +200,7 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const int sig = sig0 + sig_lane;
     const bool valid = sig < nsig;
     const int m = valid ? sig / C : 0, c = valid ? sig - m * C : 0;
-    const int64_t B = (pos[e0 + m] + 175) * FB;
+    const int64_t B = (wpos(m) + 175) * FB;
     const uint8_t* eb = win + (size_t)m * EQ * 16 + (int)(B & 15) + sel.col[c] * (int)sizeof(T);
     const uint8_t* own = eb + 16 * SEGQ * s;
     const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
@@ -281,33 +292,23 @@ bool baseline_any_supported(int fmt, int ct, int C) {
   return (size_t)EB * bstq * 16 <= 64 * 1024;
 }
 
-// Same test as the c3 kernels (fused.hip streaming_reads): the regions a kernel reads (min_spacing
-// frames per epoch) of neighbouring markers are disjoint on average; EEGFX_DMA_NT=0/1 overrides.
-static bool wide_streaming(int64_t n_frames, int64_t n, int64_t min_spacing) {
-  static const int env = [] {
-    const char* e = getenv("EEGFX_DMA_NT");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
-  return env >= 0 ? env == 1 : (n > 0 && n_frames / n >= min_spacing);
-}
-
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch) {
+                               void* scratch, int* err) {
   if (n == 0) return hipSuccess;
   int BSTQ = 0;
   const int EB = baseline_any_tile(fmt, ct, C, &BSTQ);
   const size_t lds = (size_t)EB * BSTQ * 16;
   const dim3 grid((unsigned)((n + EB - 1) / EB));
-  if (fmt == 0 && wide_streaming(n_frames, n, dev::kPre + 687))  // pre-stimulus frames unshared
+  if (fmt == 0 && streaming_reads(n_frames, n, dev::kPre + 687))  // pre-stimulus frames unshared
     hipLaunchKernelGGL((dev::baseline_any_kernel<int16_t, true>), grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
   else if (fmt == 0)
     hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
   else
     hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
   return hipGetLastError();
 }
 
@@ -322,7 +323,7 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
   if (fmt == 0 && ct == 32 && !two) {  // configs[3]: the frame size as a compile-time constant
     // streaming (non-temporal) window reads and row stores when the windows are disjoint
-    if (wide_streaming(n_frames, n, dev::kWin + 8))
+    if (streaming_reads(n_frames, n, dev::kWin + 8))
       return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
                   : launch_wide_t<int16_t, false, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
     return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out)

@@ -5,8 +5,10 @@ OffLineDataProvider.java:248-260 carries across markers and files) every selecte
 independent, so ranks take contiguous ranges of the selected-epoch list and run the fused kernel on
 their range with no data-path collective.  The only exchange is moving the per-rank feature
 matrices to their consumers, in rank order, which is the reference's list order
-(``getData()`` order).  On MI355X nodes that is one RCCL all-gather over xGMI (backend "nccl");
-the same code runs on gloo for the CPU tests.
+(``getData()`` order).  The product gather is :class:`Comm` over the C ABI (``eegfx_gather``: one
+RCCL broadcast per rank inside a group, ragged shards landing directly in their rows);
+:func:`gather_features` is the same exchange through ``torch.distributed`` (any backend -- gloo
+in the CPU tests), kept as the comparison leg of ``bench.py``.
 """
 from __future__ import annotations
 
@@ -41,6 +43,17 @@ def gather_features(local, n_total: int, group=None):
     dist.all_gather_into_tensor(full, padded, group=group)
     parts = [full[r * width: r * width + (e - s)] for r, (s, e) in enumerate(sizes)]
     return torch.cat(parts, dim=0)
+
+
+def gather_schedule(n_total: int, world: int):
+    """eegfx_gather_schedule through the C ABI: per root, (first row, row count) of the broadcast
+    eegfx_gather issues for it (host only)."""
+    import numpy as np
+    from ._lib import check, lib, ptr
+    off = np.empty(world, dtype=np.int64)
+    cnt = np.empty(world, dtype=np.int64)
+    check(lib().eegfx_gather_schedule(n_total, world, ptr(off), ptr(cnt)))
+    return [(int(o), int(c)) for o, c in zip(off, cnt)]
 
 
 def native_shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -102,15 +115,26 @@ class Comm:
         return r.value, w.value
 
     def gather(self, local, n_total: int, out=None):
+        """local: this rank's rows [e - s][cols] (float64, on the communicator's device) with
+        (s, e) = shard_range(n_total, rank, world); returns [n_total][cols] on every rank."""
         import torch
-        from ._lib import check, lib
-        _, world = self.rank_world()
+        from ._lib import lib
+        rank, world = self.rank_world()
+        s, e = shard_range(n_total, rank, world)
+        if local.dim() != 2 or local.dtype != torch.float64 or not local.is_cuda:
+            raise ValueError("local rows must be a 2-D float64 device tensor")
+        if local.shape[0] != e - s:
+            raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard of {n_total} "
+                             f"over {world} ranks is [{s}, {e})")
         cols = int(local.shape[1])
         if out is None:
             out = torch.empty((n_total, cols), dtype=torch.float64, device=local.device)
+        elif (tuple(out.shape) != (n_total, cols) or out.dtype != torch.float64
+              or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous float64 tensor of shape ({n_total}, {cols})")
         local = local.contiguous()
-        check(lib().eegfx_gather(self.handle, local.data_ptr() if local.numel() else None,
-                                 n_total, cols, out.data_ptr()))
+        self.ctx._call(1, local, lib().eegfx_gather, self.handle,
+                       local.data_ptr() if local.numel() else None, n_total, cols, out.data_ptr())
         return out
 
     def close(self) -> None:

@@ -21,7 +21,10 @@
  * `mem` argument (EEGFX_MEM_HOST: the library stages through its own device buffers and
  * returns after the results are back in host memory; EEGFX_MEM_DEVICE: pointers are HIP
  * device pointers, the work is enqueued on the context stream and the call returns without
- * synchronising -- call eegfx_ctx_synchronize()).
+ * synchronising -- call eegfx_ctx_synchronize()).  Device-resident marker positions are
+ * validated by the kernels that read them (OffLineDataProvider.java:220-225: pos-100 must lie
+ * in [0, n_frames]); a violation is reported as EEGFX_ERANGE by the next eegfx_ctx_synchronize
+ * (host positions are checked before any work is enqueued and fail the call itself).
  */
 #ifndef EEGFX_H_
 #define EEGFX_H_
@@ -63,8 +66,6 @@ extern "C" {
 /* numerics of the DWT filter bank */
 #define EEGFX_EXACT 0   /* separate fp64 mul + add in the reference order: bit-exact to Java */
 #define EEGFX_FMA 1     /* fp64 fused multiply-add: within 1e-9 relative, fewer instructions  */
-#define EEGFX_MFMA 2    /* window as one 16x512 fp64 operator on the matrix cores: within 1e-9;
-                         * falls back to EEGFX_FMA where no matrix kernel covers the layout    */
 
 typedef struct eegfx_ctx eegfx_ctx;
 typedef struct eegfx_odp eegfx_odp;
@@ -76,9 +77,14 @@ int eegfx_device_count(int* count);
 /* Creates a context on HIP device `device` with its own non-blocking stream. */
 int eegfx_ctx_create(int device, eegfx_ctx** out);
 /* Makes the context enqueue on `hip_stream` (hipStream_t, e.g. torch's current stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream.  The previous stream is drained first (the context's
+ * device buffers are allocated and released in its stream's order). */
 int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream);
-int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | _FMA | _MFMA */
+/* The stream the context currently enqueues on (hipStream_t). */
+int eegfx_ctx_stream(eegfx_ctx* ctx, void** hip_stream);
+int eegfx_ctx_set_numerics(eegfx_ctx* ctx, int numerics); /* EEGFX_EXACT (default) | EEGFX_FMA */
+/* Waits for the context's stream; EEGFX_ERANGE if a kernel enqueued since the last call met a
+ * device-resident marker position the reference would not cut (the flag is cleared). */
 int eegfx_ctx_synchronize(eegfx_ctx* ctx);
 /* Kernel timing for the roofline leg of bench.py.  While enabled, every compute call brackets its
  * dominant kernel (window_kernel for the fused path) with a pair of HIP events on the context
@@ -247,6 +253,10 @@ int eegfx_svm_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d, con
 #define EEGFX_COMM_ID_BYTES 128
 typedef struct eegfx_comm eegfx_comm;
 int eegfx_shard_range(int64_t n, int32_t rank, int32_t world, int64_t* start, int64_t* end);
+/* The schedule eegfx_gather runs: for every root r < world, the first row offsets[r] and the row
+ * count counts[r] of the broadcast rooted at r (= eegfx_shard_range of r; a root with no rows
+ * issues no broadcast).  Pure host function. */
+int eegfx_gather_schedule(int64_t n_total, int32_t world, int64_t* offsets, int64_t* counts);
 int eegfx_comm_unique_id(void* id /* EEGFX_COMM_ID_BYTES */);
 int eegfx_comm_create(eegfx_ctx* ctx, int32_t world, int32_t rank, const void* id,
                       eegfx_comm** out);
@@ -257,12 +267,6 @@ int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t
 int eegfx_group_start(void);
 int eegfx_group_end(void);
 int eegfx_comm_destroy(eegfx_comm* comm);
-
-/* The fe=dwt-8 window transform as a matrix (host only, no device): M[16][512] row-major with
- * coefficient r of WaveletTransform's first 16 (a6[0..7] ++ d6[0..7], before normalisation)
- * = sum_k M[r][k] * epoch[c][175 + k].  This is the operator EEGFX_MFMA applies on the FP64
- * matrix cores (long-double evaluation of the reference pyramid, rounded once). */
-int eegfx_dwt8_operator(double* M);
 
 /* Deterministic synthetic multiplexed int16 recording, generated on device:
  * DC -25000 counts + bounded random walk + 10 Hz sinusoid, clipped to int16.  dst is a device

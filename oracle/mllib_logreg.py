@@ -97,14 +97,18 @@ def svm_predict(X, w, intercept=0.0, threshold=0.0):
 
 
 def reference_statistics(pred, labels):
-    """(tp, tn, fp, fn) exactly as LogisticRegressionClassifier.test builds them."""
+    """(tp, tn, fp, fn) exactly as LogisticRegressionClassifier.test builds them
+    (LogisticRegressionClassifier.java:129-137).  MulticlassMetrics (Spark 1.6.2) takes its
+    ``labels`` from the actual labels only (tpByClass.keys); predicted classes outside them are
+    not in confusionMatrix."""
     pred = np.asarray(pred, dtype=np.float64)
     labels = np.asarray(labels, dtype=np.float64)
-    classes = sorted(set(labels.tolist()) | set(pred.tolist()))
+    classes = sorted(set(labels.tolist()))
     k = len(classes)
     cm = np.zeros((k, k))
     for a, p in zip(labels, pred):
-        cm[classes.index(a), classes.index(p)] += 1
+        if p in classes:
+            cm[classes.index(a), classes.index(p)] += 1
     flat = cm.flatten(order="F")  # DenseMatrix.toArray: column-major
     tn, fp, fn, tp = (int(flat[0]), int(flat[1]), int(flat[2]), int(flat[3]))
     return tp, tn, fp, fn

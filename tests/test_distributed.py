@@ -36,6 +36,24 @@ def test_native_shard_range_matches():
         native_shard_range(10, 2, 2)
 
 
+def test_gather_schedule_matches_shard_range():
+    """eegfx_gather_schedule (the per-root broadcast plan eegfx_gather runs) against shard_range,
+    ragged n over 1..8 ranks: offsets are the shard starts, counts the shard sizes, and the plan
+    covers [0, n) in rank (= getData()) order."""
+    import eeg_dataanalysispackage_amd as fx
+    from eeg_dataanalysispackage_amd.sharding import gather_schedule
+    for n in (0, 1, 5, 7, 8, 9, 63, 64, 65, 1_000_003, 64_000_000, 64_000_007):
+        for world in range(1, 9):
+            plan = gather_schedule(n, world)
+            assert plan == [(s, e - s) for s, e in (shard_range(n, r, world) for r in range(world))]
+            assert sum(c for _, c in plan) == n
+            assert all(o1 + c1 == o2 for (o1, c1), (o2, _) in zip(plan, plan[1:]))
+    with pytest.raises(fx.EegfxError):
+        gather_schedule(10, 0)
+    with pytest.raises(fx.EegfxError):
+        gather_schedule(-1, 2)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -65,6 +83,41 @@ def _worker(rank, world, port, n, out_dir):
         np.save(os.path.join(out_dir, "ok.npy"), np.array([np.array_equal(full, ref)]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _schedule_worker(rank, world, port, n, out_dir):
+    """eegfx_gather's collective pattern rehearsed on gloo: for every root of
+    eegfx_gather_schedule one broadcast of that root's rows into out[offset : offset + count]
+    (ncclBroadcast in eegfx_gather, dist.broadcast here); roots without rows issue nothing."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eeg_dataanalysispackage_amd.sharding import gather_schedule
+    cols = 48
+    full_ref = torch.arange(n * cols, dtype=torch.float64).reshape(n, cols)
+    s, e = shard_range(n, rank, world)
+    local = full_ref[s:e].clone()
+    out = torch.full((n, cols), float("nan"), dtype=torch.float64)
+    for root, (off, cnt) in enumerate(gather_schedule(n, world)):
+        if cnt == 0:
+            continue
+        buf = local if root == rank else out[off:off + cnt]
+        buf = buf.contiguous()
+        dist.broadcast(buf, src=root)
+        out[off:off + cnt] = buf
+    np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([torch.equal(out, full_ref)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(3, 7), (4, 2), (2, 37)])
+def test_gather_schedule_broadcasts_world_n(tmp_path, world, n):
+    import torch.multiprocessing as mp
+    mp.spawn(_schedule_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world,
+             join=True)
+    assert all(bool(np.load(tmp_path / f"ok{r}.npy")[0]) for r in range(world))
 
 
 @pytest.mark.parametrize("n", [37, 64])

@@ -178,31 +178,6 @@ def test_channel_name_escape_and_order(tmpdata):
     assert oerr == "ChannelNotFound: [3, 2, 1]" or oerr == ""
 
 
-# ---- the dwt-8 window operator behind the "mfma" numerics (host only) ---------------------------
-def test_dwt8_operator_matches_oracle_features():
-    """normalise(M @ window) == the oracle's fe=dwt-8 features (WaveletTransform.java:107-141)."""
-    M = fx.dwt8_operator()
-    assert M.shape == (16, 512)
-    rng = np.random.default_rng(17)
-    raw = np.clip(-25000 + np.cumsum(rng.integers(-40, 41, size=(30000, 3)), axis=0),
-                  -32768, 32767).astype(np.int16)
-    pos = rng.integers(100, 29000, size=64)
-    ep = oracle.decode_epochs(raw, [0, 1, 2], [0.1] * 3, pos)
-    want = oracle.extract_features(ep)
-    coef = np.einsum("rk,nck->ncr", M, ep[:, :, 175:687]).reshape(len(pos), 48)
-    got = coef / np.linalg.norm(coef, axis=1, keepdims=True)
-    assert np.max(np.abs(got - want)) < 1e-12
-
-
-def test_dwt8_operator_is_block_circulant():
-    """M[r][k] = M[8(r>>3)][(k - 64(r&7)) mod 512]: the identity mfma.hip uses to keep only rows
-    a6[0] and d6[0] in LDS."""
-    M = fx.dwt8_operator()
-    for r in range(16):
-        row0 = M[8 * (r >> 3)]
-        np.testing.assert_allclose(M[r], np.roll(row0, 64 * (r & 7)), rtol=0, atol=1e-15)
-
-
 def test_vectorized_orientation_reads_as_multiplexed(tmp_path):
     """A DataOrientation=VECTORIZED copy of DoD2015_01 (channel after channel) reads back as the
     multiplexed original; the planning provider sees the same epochs.  Parity unpinned against

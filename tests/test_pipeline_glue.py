@@ -45,6 +45,12 @@ def test_reference_statistics_mapping():
     import pytest
     with pytest.raises(IndexError):
         reference_statistics([1, 1], [1, 1])
+    # MulticlassMetrics.labels are the actual classes only: a single actual class with mixed
+    # predictions is still a 1x1 matrix, and the reference's cm[1] throws
+    with pytest.raises(IndexError):
+        reference_statistics([0, 1, 1], [0, 0, 0])
+    with pytest.raises(IndexError):
+        ref.reference_statistics([0, 1, 1], [0, 0, 0])
 
 
 def test_mllib_restatement_basics():

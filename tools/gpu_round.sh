@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round evidence on one GPU box: parity tests -> smoke -> bench (fma headline, exact alt) ->
 # rocprofv3 kernel trace + stats of the bench -> PMC FETCH_SIZE / WRITE_SIZE passes on
-# window_kernel (one counter per pass, kernel trace only) -> traffic summaries.
+# window_kernel (one counter per pass, kernel trace only) -> traffic summaries -> extra workloads.
 # Every GPU step has its own time limit; the chain stops at the first failure.
+#   TAG=r02a TESTS=1 NUMS="fma exact" EXTRA="c32 stream dropin big" bash tools/gpu_round.sh
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -12,17 +13,19 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ "${TESTS:-1}" = "1" ]; then
   echo "== pytest -m gpu"; date
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
   tail -3 "$OUT/pytest_gpu.log"
   echo "== smoke"; date
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
   cat "$OUT/smoke.log"
 fi
-echo "== bench"; date
-timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
-cat "$OUT/bench.json"
+if [ "${BENCH:-1}" = "1" ]; then
+  echo "== bench"; date
+  timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+  cat "$OUT/bench.json"
+fi
 cd /tmp
-for NUM in ${NUMS:-fma exact}; do
+for NUM in ${NUMS:-fma}; do
   echo "== rocprofv3 kernel trace $NUM"; date
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$NUM" -o run -- python3 "$ROOT/bench.py" --numerics $NUM --cpu-sample 0 --alt-steps 0 > "$OUT/trace_$NUM.log" 2>&1 || { tail -30 "$OUT/trace_$NUM.log"; exit 1; }
   tail -1 "$OUT/trace_$NUM.log"
@@ -36,9 +39,13 @@ for NUM in ${NUMS:-fma exact}; do
     --algorithmic-bytes 3476000000 --out "$OUT/traffic_$NUM.json"
 done
 cd "$ROOT"
-for WL in ${EXTRA:-c32 stream logreg svm}; do
+for WL in ${EXTRA:-c32 stream dropin big}; do
   echo "== bench $WL"; date
-  timeout -k 10 400 python bench.py --workload $WL > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err" || { tail -30 "$OUT/bench_$WL.err"; exit 1; }
+  if [ "$WL" = "big" ]; then  # configs[2]: one rank's 8M-epoch shard (48 GB recording)
+    timeout -k 10 400 python bench.py --epochs 8000000 --steps 20 --warmup 10 --cpu-sample 0 --alt-steps 3 > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err" || { tail -30 "$OUT/bench_$WL.err"; exit 1; }
+  else
+    timeout -k 10 400 python bench.py --workload $WL > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err" || { tail -30 "$OUT/bench_$WL.err"; exit 1; }
+  fi
   cat "$OUT/bench_$WL.json"
 done
 echo "== done"; date
