@@ -194,6 +194,49 @@ __device__ __forceinline__ void level1_jit(Fetch fetch, float r, float b, double
   }
 }
 
+// level1_jit with only the lane's own 64 samples decoded: the 8 halo samples [64(s+1), 64(s+1)+8)
+// are the fp32 values lane s+1 of the group decoded first, fetched with ds_bpermute (one dword
+// each) and widened here -- 8 fewer decodes per lane (fma numerics: 2 % fewer VALU instructions,
+// ~1 % faster; under EXACT the longer live range of y0 cost more than it saved).
+template <bool FAST, typename Fetch>
+__device__ __forceinline__ void level1_jit_halo(Fetch fetch, float r, float b, int gbase, int s,
+                                                double (&a1)[40]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  const int src = gbase + ((s + 1) & (kLanesPerSignal - 1));
+  double x[kIn];
+  float y0[8];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {  // output i reads x[2i .. 2i+9]
+#pragma unroll
+    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
+      if (k < kSegLen) {
+        const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
+        const dwt8_f32x2 y = v * rr - bb;
+        if (k < 8) {
+          y0[k] = y.x;
+          y0[k + 1] = y.y;
+        }
+        x[k] = (double)y.x;
+        x[k + 1] = (double)y.y;
+      } else {
+        x[k] = (double)__shfl(y0[k - kSegLen], src, 64);
+        x[k + 1] = (double)__shfl(y0[k + 1 - kSegLen], src, 64);
+      }
+    }
+    a1[i] = fir10<FAST, false>(x + 2 * i);
+  }
+}
+
+// 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps
+// (relative error ~1e-16, inside the 1e-9 contract); v = 0 gives inf, so an all-zero row still
+// normalises to NaN as the reference's 0/0 does.
+__device__ __forceinline__ double rsqrt_nr(double v) {
+  double r = __builtin_amdgcn_rsq(v);
+  r = r * __builtin_fma(-0.5 * v * r, r, 1.5);
+  r = r * __builtin_fma(-0.5 * v * r, r, 1.5);
+  return r;
+}
+
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
 // xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
 // Returns a6[s] and d6[s].

@@ -94,13 +94,13 @@ __global__ __launch_bounds__(256) void features_from_epochs_kernel(const double*
                                                                    int64_t n, int C, int skip,
                                                                    int nfeat, int row_stride,
                                                                    double* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+  extern __shared__ __attribute__((aligned(16))) double fsmem[];
   const int nw = blockDim.x / 64;
   const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
   const int el = lane >> 3, s = lane & 7;
   const int F = C * nfeat;
-  double* xch = smem + w * 64 * kSlot;
-  double* feat = smem + nw * 64 * kSlot;  // [8][F]
+  double* xch = fsmem + w * 64 * kSlot;
+  double* feat = fsmem + nw * 64 * kSlot;  // [8][F]
   double* norm = feat + 8 * F;            // [8]
   const int64_t e0 = (int64_t)blockIdx.x * 8;
   const int64_t e = e0 + el;

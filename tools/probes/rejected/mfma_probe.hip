@@ -6,7 +6,7 @@
 #include <cstdio>
 #include <vector>
 
-#include "../../eeg_dataanalysispackage_amd/csrc/mfma.hip"
+#include "mfma.hip"
 
 int main() {
   const int64_t n = 1000000, nf = 1000 * n + 2000;

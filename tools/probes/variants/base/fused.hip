@@ -192,16 +192,12 @@ __device__ __forceinline__ int64_t window_byte(const int64_t* __restrict__ pos, 
 // (DataProviderUtils.java:49-59, Baseline.java:39-41), two samples at a time with packed fp32
 // math, read straight from the staged window: own[k*CT] for k < 64, then the 8 halo samples
 // nxt[k*CT] of the next segment.
-// FMA numerics: the 8 halo samples come from lane s+1 as decoded fp32 values (level1_jit_halo).
 template <int CT, bool FAST>
 __device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nxt, float r, float b,
-                                           int gbase, int s, double (&a1)[40]) {
-  if constexpr (FAST)
-    level1_jit_halo<FAST>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a1);
-  else
-    level1_jit<FAST>(
-        [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r,
-        b, a1);
+                                           double (&a1)[40]) {
+  level1_jit<FAST>(
+      [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r, b,
+      a1);
 }
 
 // SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
@@ -210,8 +206,8 @@ __device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nx
 //   EXACT: lane e < ne folds Math.pow(f, 2) over row e in index order (the 8 dependent chains run
 //          side by side), then the 64 lanes divide and store (16-byte stores).
 //   FMA:   (1e-9 contract) the 8 lanes of an epoch each square-sum F/8 features, a 3-step
-//          butterfly completes the row sum, and the row is scaled by 1/sqrt (rsqrt_nr: within an
-//          ulp or two of x / s; an all-zero row still gives NaN = 0 * inf); the scaled rows go
+//          butterfly completes the row sum, and the row is scaled by one reciprocal (x * (1/s) is
+//          within 1 ulp of x / s; an all-zero row still gives NaN = 0 * inf); the scaled rows go
 //          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
 //          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).
 template <int F, bool FAST>
@@ -232,7 +228,7 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
-    const double inv = rsqrt_nr(acc);
+    const double inv = 1.0 / sqrt(acc);
     if (e < ne) {
 #pragma unroll
       for (int i = 0; i < P; i += 2)
@@ -386,7 +382,7 @@ __global__ __launch_bounds__(64 * C, 4) void window_kernel(
   const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
   const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
   double a1[40], a6, d6;
-  level1_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a1);
+  level1_lds<CT, FAST>(own, nxt, r, b, a1);
   halo<32, true>(a1, nullptr, lane & ~7, s);
   dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
 

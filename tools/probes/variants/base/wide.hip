@@ -207,13 +207,9 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const float r = sel.res[c];
     const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
     double a1[40], a6, d6;
-    if constexpr (FAST)  // the 8 lanes of a group share the signal: halo samples from lane s+1
-      level1_jit_halo<FAST>([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
-                            a1);
-    else
-      level1_jit<FAST>(
-          [&](int k) { return sample_at<T>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
-          r, b, a1);
+    level1_jit<FAST>(
+        [&](int k) { return sample_at<T>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
+        r, b, a1);
     halo<32, true>(a1, nullptr, lane & ~7, s);
     dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
     if (valid) {
@@ -230,7 +226,7 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
       double acc = 0.0;
       for (int i = lane; i < F; i += 64) acc = __builtin_fma(feat[m * F + i], feat[m * F + i], acc);
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) norm[m] = rsqrt_nr(acc);  // the reciprocal norm (multiplied below)
+      if (lane == 0) norm[m] = sqrt(acc);
     }
   } else {
     // the reference's sequential fold, index order, one lane per epoch
@@ -246,118 +242,9 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   __syncthreads();
   double* o = out + e0 * F;
   for (int i = tid; i < ne * F; i += blockDim.x) {
-    const double v = FAST ? feat[i] * norm[i / F] : feat[i] / norm[i / F];
+    const double v = feat[i] / norm[i / F];
     if constexpr (STREAM) __builtin_nontemporal_store(v, o + i);
     else o[i] = v;
-  }
-}
-
-// configs[3]: the full 32-channel int16 montage with every channel through the DWT (512-dim rows),
-// one epoch per workgroup of 4 waves (wave w = channels 8w..8w+7, lane = (channel, segment)).
-// Everything the generic kernel computes from runtime sizes is constexpr here: the staging rows
-// (wave w issues rows w, w+4, ...; quad i = 257 sg + rem of the window lands at byte offset
-// 4096 sg + 16 rem, and the lane's (sg, rem) advance incrementally by 256 quads per row), the
-// signal -> channel map (shifts) and the row normalisation (FMA: rsqrt_nr, one multiply per
-// feature; EXACT keeps the reference's sequential sum and division).  Measured against the
-// generic kernel at FB = 64 (tools/probes, 666 launches of 250k epochs): 2.58 -> 2.46 ms,
-// 1,114 -> 1,040 VALU instructions per wave.
-template <bool FAST, bool STREAM>
-__global__ __launch_bounds__(256) void window_c32_kernel(
-    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
-    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
-    double* __restrict__ out) {
-  constexpr int C = 32, FB = 64, SEGQ = 4 * FB + 1, EQ = 8 * SEGQ, F = 16 * C;
-  constexpr int NROWS = (EQ + 63) / 64;  // 33
-  __shared__ __attribute__((aligned(16))) uint8_t win[EQ * 16];
-  __shared__ __attribute__((aligned(16))) double feat[F];
-  __shared__ double norm1;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t nbytes = n_frames * FB;
-  const int64_t p0 = pos[e];
-  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : (int64_t)kPre;  // flagged by baselines
-  const int64_t B = (p + 175) * FB;
-  const int64_t Bq = B & ~(int64_t)15;
-  constexpr int64_t span = (int64_t)64 * FB * 7 + 16 * SEGQ;
-  const bool full = Bq >= 0 && Bq + span <= nbytes;
-  const uint8_t* sb = raw + Bq;
-  // row j = w + 4t, quad i = 64 j + lane = sg * SEGQ + rem
-  int i = 64 * w + lane;
-  int sg = i / SEGQ;
-  int rem = i - sg * SEGQ;
-#pragma unroll
-  for (int t = 0; t < (NROWS + 3) / 4; ++t) {
-    const int j = w + 4 * t;
-    if (j < NROWS) {  // uniform
-      const uint32_t off = (uint32_t)(64 * FB * sg + 16 * rem);
-      uint8_t* dst = win + (size_t)(64 * j) * 16;
-      if (64 * j + lane < EQ) {
-        if (full || (Bq + off >= 0 && Bq + off + 16 <= nbytes)) {
-          dma16_s<STREAM>(sb, off, dst);
-        } else {
-          const wq_a4 v = wide_load16(raw, nbytes, Bq + off);
-          uint32_t* d = (uint32_t*)(dst + 16 * lane);
-          d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
-      }
-      // next row: i += 256 (SEGQ = 257): the segment advances unless rem was 0
-      const bool adv = rem >= 1;
-      sg += adv ? 1 : 0;
-      rem = adv ? rem - 1 : 256;
-    }
-  }
-  dma_drain();
-  __syncthreads();
-
-  const int c = w * 8 + (lane >> 3), s = lane & 7;
-  const uint8_t* eb = win + (int)(B & 15) + sel.col[c] * 2;
-  const uint8_t* own = eb + 16 * SEGQ * s;
-  const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
-  const float r = sel.res[c];
-  const float b = base[e * C + c];
-  double a1[40], a6, d6;
-  if constexpr (FAST)
-    level1_jit_halo<FAST>([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7,
-                          s, a1);
-  else
-    level1_jit<FAST>(
-        [&](int k) { return sample_at<int16_t>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
-        r, b, a1);
-  halo<32, true>(a1, nullptr, lane & ~7, s);
-  dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
-  feat[c * 16 + s] = a6;
-  feat[c * 16 + 8 + s] = d6;
-  __syncthreads();
-  double* o = out + e * F;
-  if constexpr (FAST) {
-    if (w == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < F / 64; ++k) acc = __builtin_fma(feat[lane + 64 * k], feat[lane + 64 * k], acc);
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) norm1 = rsqrt_nr(acc);
-    }
-    __syncthreads();
-    const double inv = norm1;
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    const f64x2 v = *(const f64x2*)(feat + 2 * tid);
-    const f64x2 q = {v.x * inv, v.y * inv};
-    if constexpr (STREAM) __builtin_nontemporal_store(q, (f64x2*)(o + 2 * tid));
-    else *(f64x2*)(o + 2 * tid) = q;
-  } else {
-    if (tid == 0) {
-      double acc = 0.0;
-      for (int k = 0; k < F; ++k) acc = acc + feat[k] * feat[k];
-      norm1 = sqrt(acc);
-    }
-    __syncthreads();
-    const double nv = norm1;
-    for (int k = tid; k < F; k += 256) {
-      const double v = feat[k] / nv;
-      if constexpr (STREAM) __builtin_nontemporal_store(v, o + k);
-      else o[k] = v;
-    }
   }
 }
 
@@ -434,18 +321,7 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
 #define EEGFX_W(T, FA)                                                                        \
   return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out)       \
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
-  if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) {  // configs[3]
-    const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
-    const dim3 g((unsigned)n);
-#define EEGFX_C32(FA, NTV) \
-    hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV>), g, dim3(256), 0, st, (const uint8_t*)raw, \
-                       n_frames, sel, pos, base, n, out)
-    if (fast) { if (nt) EEGFX_C32(true, true); else EEGFX_C32(true, false); }
-    else { if (nt) EEGFX_C32(false, true); else EEGFX_C32(false, false); }
-#undef EEGFX_C32
-    return hipGetLastError();
-  }
-  if (fmt == 0 && ct == 32 && !two) {  // the frame size as a compile-time constant
+  if (fmt == 0 && ct == 32 && !two) {  // configs[3]: the frame size as a compile-time constant
     // streaming (non-temporal) window reads and row stores when the windows are disjoint
     if (streaming_reads(n_frames, n, dev::kWin + 8))
       return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out)

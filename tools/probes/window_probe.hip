@@ -1,70 +1,80 @@
-// Probe: window_kernel (VALU cascade, fma numerics) timing under EEGFX_FUSED_ABLATION (bit 0: no
-// window DMA, bit 1: no LDS reads/decode, bit 2: no filter bank) on the bench workload.
+// Probe: window_kernel (the fused c3 path) or window_wide_kernel (configs[3]) timed under sustained
+// load, for A/B studies of kernel variants.  FUSED_SRC / WIDE_SRC name the kernel source to build
+// against (default: the product files); a variant is a modified copy under tools/probes/variants/.
+//
+//   hipcc ... -DFUSED_SRC='"variants/v1/fused.hip"' window_probe.hip -o window_probe_v1
+//   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
+//
+// Inputs are the bench workload: synth_kernel recording (configs[1]: 1M epochs x 3 ch, or
+// configs[3]: 250k epochs x 32 ch), one marker every 1,000 frames.  Prints the average launch time
+// over PROBE_ITERS launches after 200 warm-up launches (the clock settles under the power cap),
+// and a checksum of the feature matrix (sum and sum of squares) for a quick equality check
+// between variants.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
-#include "../../eeg_dataanalysispackage_amd/csrc/fused.hip"
-
-__global__ void fill_random(uint32_t* p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z ^= z >> 27;
-    p[i] = (uint32_t)z & 0x0FFF0FFFu;  // two int16 samples in [0, 4096)
-  }
-}
+#ifndef FUSED_SRC
+#define FUSED_SRC "../../eeg_dataanalysispackage_amd/csrc/fused.hip"
+#endif
+#ifndef WIDE_SRC
+#define WIDE_SRC "../../eeg_dataanalysispackage_amd/csrc/wide.hip"
+#endif
+#include FUSED_SRC
+#include WIDE_SRC
+#include "../../eeg_dataanalysispackage_amd/csrc/kernels.hip"
 
 int main() {
-  const int64_t n = 1000000, nf = 1000 * n + 2000;
-  uint8_t* raw;
+  const bool wide = getenv("PROBE_WIDE") != nullptr;
+  const bool fast = getenv("PROBE_EXACT") == nullptr;
+  const int ct = wide ? 32 : 3;
+  const int64_t n = wide ? 250000 : 1000000, nf = 1000 * n + 2000;
+  int16_t* raw;
   int64_t* pos;
   float* base;
   double* out;
-  (void)hipMalloc(&raw, nf * 6);
+  (void)hipMalloc(&raw, nf * ct * 2);
   (void)hipMalloc(&pos, n * 8);
-  (void)hipMalloc(&base, n * 12);
-  (void)hipMalloc(&out, n * 48 * 8);
-  if (getenv("PROBE_RANDOM")) fill_random<<<4096, 256>>>((uint32_t*)raw, nf * 6 / 4);
-  else (void)hipMemset(raw, 3, nf * 6);
+  (void)hipMalloc(&base, n * ct * 4);
+  (void)hipMalloc(&out, n * 16 * ct * 8);
+  (void)eegfx::launch_synth(0, raw, nf, ct, 0x5EED);
   std::vector<int64_t> hp(n);
-  const char* sp = getenv("PROBE_SPACING");  // frames between markers (1000: the bench)
-  const int64_t spacing = sp ? atoi(sp) : 1000;
-  for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + spacing * i;
+  for (int64_t i = 0; i < n; ++i) hp[i] = 1000 + 1000 * i;
   (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
   eegfx::ChanSel sel{};
-  for (int c = 0; c < 3; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
-  (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
+  for (int c = 0; c < ct; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
+  auto baseline = [&] {
+    if (wide) (void)eegfx::launch_baseline_any(0, raw, 0, nf, ct, sel, ct, pos, n, base, nullptr);
+    else (void)eegfx::launch_fused_baseline(0, raw, nf, ct, sel, ct, pos, n, base, nullptr);
+  };
+  auto window = [&] {
+    if (wide) (void)eegfx::launch_window_wide(0, raw, 0, nf, ct, sel, ct, pos, n, fast, base, out);
+    else (void)eegfx::launch_fused_window(0, raw, nf, ct, sel, ct, pos, n, fast, base, out);
+  };
+  baseline();
+  const char* it = getenv("PROBE_ITERS");
+  const int iters = it ? atoi(it) : 2000;
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  for (int r = 0; r < 2; ++r)
-    (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, !getenv("PROBE_EXACT"), base, out);
-  if (getenv("PROBE_BASELINE")) {  // time the baseline kernel instead of the window kernel
-    hipEvent_t c, d;
-    (void)hipEventCreate(&c);
-    (void)hipEventCreate(&d);
-    for (int r = 0; r < 50; ++r) (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
-    (void)hipEventRecord(c);
-    for (int r = 0; r < 500; ++r) (void)eegfx::launch_fused_baseline(0, raw, nf, 3, sel, 3, pos, n, base);
-    (void)hipEventRecord(d);
-    (void)hipEventSynchronize(d);
-    float bms;
-    (void)hipEventElapsedTime(&bms, c, d);
-    printf("baseline ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, bms / 500);
-    return 0;
-  }
-  const char* it = getenv("PROBE_ITERS");
-  const int iters = it ? atoi(it) : 10;
+  const bool time_baseline = getenv("PROBE_BASELINE") != nullptr;
+  for (int r = 0; r < 200; ++r) time_baseline ? baseline() : window();
   (void)hipEventRecord(a);
-  for (int r = 0; r < iters; ++r)
-    (void)eegfx::launch_fused_window(0, raw, nf, 3, sel, 3, pos, n, !getenv("PROBE_EXACT"), base, out);
+  for (int r = 0; r < iters; ++r) time_baseline ? baseline() : window();
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms;
   (void)hipEventElapsedTime(&ms, a, b);
-  printf("window ablation %d: %.4f ms\n", EEGFX_FUSED_ABLATION, ms / iters);
-  return 0;
+  window();
+  std::vector<double> h(n * 16 * ct);
+  (void)hipMemcpy(h.data(), out, h.size() * 8, hipMemcpyDeviceToHost);
+  double s = 0, q = 0;
+  for (double v : h) { s += v; q += v * v; }
+  const hipError_t e = hipGetLastError();
+  printf("%s %s %s: %.4f ms per launch (%d launches)  checksum %.17g %.17g  %s\n",
+         wide ? "wide c32" : "window c3", fast ? "fma" : "exact",
+         time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
+  return e == hipSuccess ? 0 : 1;
 }
