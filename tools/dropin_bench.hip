@@ -1,0 +1,203 @@
+// dropin_bench -- configs[0]'s per-epoch drop-in through the C ABI, timed natively (what a JNI
+// caller of IFeatureExtraction.extractFeatures sees, without Python in the loop).
+//
+//   dropin_bench <repo> [reps] [numerics: 0 exact | 1 fma]
+//
+// Loads DoD2015_01 through the ABI (eegfx_read_header / _read_raw / _read_markers /
+// _plan_markers / _cut_epochs_f64: the 11 infoTrain epochs), then:
+//   single   one thread, one context: eegfx_extract_features_f64 on one host epoch per call
+//            (FeatureExtractionTest.java:62-67 and the Spark map closure make exactly this call);
+//   threads  T threads, one context each (include/eegfx.h's rule for Spark executor threads),
+//            all calling concurrently;
+//   cpu      the oracle's C restatement (oracle/liboracle.so, full pyramid) on the same epoch,
+//            one thread -- the per-thread rate of the CPU baseline;
+//   sync     the floor of one launch round trip on this box: an empty kernel + hipStreamSynchronize,
+//            and the same with a spin on hipEventQuery.
+// Prints one JSON object.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "eegfx.h"
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    int _rc = (x);                                                               \
+    if (_rc != 0) {                                                              \
+      fprintf(stderr, "%s failed: %d %s\n", #x, _rc, eegfx_last_error());        \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+static std::vector<double> g_epochs;  // [11][3][750]
+static int g_numerics = 1;
+
+struct Lat {
+  double med, p99;
+};
+static Lat stats(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return {v[v.size() / 2], v[(size_t)(v.size() * 0.99)]};
+}
+
+struct Job {
+  int reps;
+  double per_call;
+  int rc;
+};
+static void* worker(void* arg) {
+  Job* j = (Job*)arg;
+  eegfx_ctx* ctx = nullptr;
+  j->rc = eegfx_ctx_create(0, &ctx);
+  if (j->rc) return nullptr;
+  eegfx_ctx_set_numerics(ctx, g_numerics);
+  double out[48];
+  for (int i = 0; i < 20; ++i)
+    eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out, EEGFX_MEM_HOST);
+  const double t0 = now_s();
+  for (int i = 0; i < j->reps; ++i)
+    j->rc |= eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)(i % 11) * 2250, 1, 3, 8,
+                                        512, 175, 16, out, EEGFX_MEM_HOST);
+  j->per_call = (now_s() - t0) / j->reps;
+  eegfx_ctx_destroy(ctx);
+  return nullptr;
+}
+
+__global__ void empty_kernel(int* p) {
+  if (p && threadIdx.x == 1024) *p = 0;
+}
+
+int main(int argc, char** argv) {
+  const std::string repo = argc > 1 ? argv[1] : ".";
+  const int reps = argc > 2 ? atoi(argv[2]) : 2000;
+  g_numerics = argc > 3 ? atoi(argv[3]) : 1;
+  const std::string base = repo + "/tests/golden/test-data/DoD/DoD2015_01";
+  eegfx_header_info hi;
+  CK(eegfx_read_header((base + ".vhdr").c_str(), &hi, nullptr, 0));
+  int64_t nf = 0;
+  CK(eegfx_recording_frames((base + ".vhdr").c_str(), (base + ".eeg").c_str(), &nf));
+  std::vector<int16_t> raw((size_t)nf * hi.n_channels);
+  CK(eegfx_read_raw(nullptr, (base + ".vhdr").c_str(), (base + ".eeg").c_str(), raw.data(),
+                    (int64_t)raw.size() * 2, EEGFX_MEM_HOST));
+  int64_t nm = 0;
+  CK(eegfx_read_markers((base + ".vmrk").c_str(), nullptr, 0, &nm));
+  std::vector<eegfx_marker> mk((size_t)nm);
+  CK(eegfx_read_markers((base + ".vmrk").c_str(), mk.data(), nm, &nm));
+  std::vector<int64_t> pos((size_t)nm);
+  std::vector<double> lab((size_t)nm);
+  int64_t bal = 0, k = 0;
+  CK(eegfx_plan_markers(mk.data(), nm, nf, 1, &bal, pos.data(), lab.data(), &k));
+  eegfx_ctx* ctx = nullptr;
+  CK(eegfx_ctx_create(0, &ctx));
+  CK(eegfx_ctx_set_numerics(ctx, g_numerics));
+  const int32_t cols[3] = {0, 1, 2};
+  const float res[3] = {0.1f, 0.1f, 0.1f};
+  g_epochs.resize((size_t)k * 3 * 750);
+  CK(eegfx_cut_epochs_f64(ctx, raw.data(), EEGFX_INT_16, nf, hi.n_channels, cols, res, 3,
+                          pos.data(), k, g_epochs.data(), EEGFX_MEM_HOST));
+
+  // single thread, one epoch per call
+  double out[48];
+  for (int i = 0; i < 50; ++i)
+    CK(eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                  EEGFX_MEM_HOST));
+  std::vector<double> lat;
+  for (int i = 0; i < reps; ++i) {
+    const double t0 = now_s();
+    CK(eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)(i % k) * 2250, 1, 3, 8, 512,
+                                  175, 16, out, EEGFX_MEM_HOST));
+    lat.push_back(now_s() - t0);
+  }
+  const Lat single = stats(lat);
+  // the 11 epochs as one batch
+  std::vector<double> out11((size_t)k * 48);
+  lat.clear();
+  for (int i = 0; i < reps / 4; ++i) {
+    const double t0 = now_s();
+    CK(eegfx_extract_features_f64(ctx, g_epochs.data(), k, 3, 8, 512, 175, 16, out11.data(),
+                                  EEGFX_MEM_HOST));
+    lat.push_back(now_s() - t0);
+  }
+  const Lat batch = stats(lat);
+
+  // launch round-trip floors
+  hipStream_t st;
+  (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  hipEvent_t ev;
+  (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  std::vector<double> ls, le;
+  for (int i = 0; i < reps; ++i) {
+    double t0 = now_s();
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, nullptr);
+    (void)hipStreamSynchronize(st);
+    ls.push_back(now_s() - t0);
+    t0 = now_s();
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, nullptr);
+    (void)hipEventRecord(ev, st);
+    while (hipEventQuery(ev) == hipErrorNotReady) {
+    }
+    le.push_back(now_s() - t0);
+  }
+  const Lat sync_floor = stats(ls), spin_floor = stats(le);
+
+  // T threads, own contexts
+  printf("{\"single_epoch\": {\"median_us\": %.2f, \"p99_us\": %.2f, \"epochs_per_s\": %.1f},\n",
+         single.med * 1e6, single.p99 * 1e6, 1.0 / single.med);
+  printf(" \"batch_11\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f},\n", batch.med * 1e6,
+         k / batch.med);
+  printf(" \"launch_floor\": {\"empty_kernel_stream_sync_us\": %.2f, \"empty_kernel_event_spin_us\": %.2f},\n",
+         sync_floor.med * 1e6, spin_floor.med * 1e6);
+  printf(" \"threads\": {");
+  const int Ts[3] = {2, 4, 8};
+  for (int ti = 0; ti < 3; ++ti) {
+    const int T = Ts[ti];
+    std::vector<pthread_t> th((size_t)T);
+    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0});
+    for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
+    double agg = 0, mean = 0;
+    int rc = 0;
+    for (int t = 0; t < T; ++t) {
+      pthread_join(th[(size_t)t], nullptr);
+      agg += 1.0 / jobs[(size_t)t].per_call;
+      mean += jobs[(size_t)t].per_call / T;
+      rc |= jobs[(size_t)t].rc;
+    }
+    printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, \"rc\": %d}",
+           ti ? ", " : "", T, 1.0 / mean, agg, rc);
+  }
+  printf("},\n");
+
+  // the C port, one thread
+  void* h = dlopen((repo + "/oracle/liboracle.so").c_str(), RTLD_NOW);
+  double cpu_med = 0;
+  if (h) {
+    typedef void (*fe_t)(const double*, int64_t, int32_t, int32_t, int32_t, int32_t, int32_t,
+                         double*);
+    fe_t fe = (fe_t)dlsym(h, "oracle_extract_features");
+    if (fe) {
+      for (int i = 0; i < 50; ++i) fe(g_epochs.data(), 1, 3, 175, 512, 16, 1, out);
+      lat.clear();
+      for (int i = 0; i < reps; ++i) {
+        const double t0 = now_s();
+        fe(g_epochs.data() + (size_t)(i % k) * 2250, 1, 3, 175, 512, 16, 1, out);
+        lat.push_back(now_s() - t0);
+      }
+      cpu_med = stats(lat).med;
+    }
+  }
+  printf(" \"cpu_port_single_thread\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f}}\n",
+         cpu_med * 1e6, cpu_med > 0 ? 1.0 / cpu_med : 0.0);
+  eegfx_ctx_destroy(ctx);
+  return 0;
+}
