@@ -698,21 +698,20 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
       const size_t row_w = sizeof(double) * EEGFX_DWT8_EPOCH_SIZE;
       const size_t row_p = sizeof(double) * EEGFX_POSTSTIMULUS;
       const uint8_t* src = (const uint8_t*)epochs + sizeof(double) * (size_t)skip;
-      if ((size_t)n * C * row_w <= kZeroCopyBytes) {
+      if ((size_t)n * C * row_w <= kZeroCopyBytes && features_small_supported(C)) {
         // Small batches (a single epoch above all): latency, not bandwidth.  The window rows are
-        // packed into a pinned, device-mapped buffer by the calling thread and the kernel reads
-        // them -- and writes the rows -- across the host link directly: one launch and one stream
-        // sync, no DMA transfers (each costs a copy-engine round trip) and no allocation once the
-        // context's staging has grown.
+        // packed into a pinned, device-mapped buffer by the calling thread and the kernel
+        // (features_small_kernel) reads them -- and writes the rows -- across the host link
+        // directly: one launch and one stream sync, no DMA transfers (each costs a copy-engine
+        // round trip) and no allocation once the context's staging has grown.
         double* hin = (double*)ctx->pin_in.get((size_t)n * C * row_w);
         double* hout = (double*)ctx->pin_out.get(out_bytes);
         for (int64_t r = 0; r < n * C; ++r)
           memcpy((uint8_t*)hin + (size_t)r * row_w, src + (size_t)r * row_p, row_w);
         ctx->tic();
-        HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)ctx->pin_in.device_ptr(),
-                                              n, C, 0, feature_size, ctx->numerics != EEGFX_EXACT,
-                                              (double*)ctx->pin_out.device_ptr(),
-                                              EEGFX_DWT8_EPOCH_SIZE));
+        HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
+                                        feature_size, ctx->numerics != EEGFX_EXACT,
+                                        (double*)ctx->pin_out.device_ptr()));
         ctx->toc(0);
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
         memcpy(out, hout, out_bytes);

@@ -132,6 +132,63 @@ __global__ __launch_bounds__(256) void features_from_epochs_kernel(const double*
     out[e0 * F + idx] = feat[idx] / norm[idx / F];
 }
 
+// a11..a13 for small host batches (the per-epoch IFeatureExtraction drop-in): one workgroup per
+// epoch reads the epoch's packed window rows (C x 512 doubles, pinned host memory mapped into the
+// device) with 16-byte loads, all issued before the first wait -- one host-link round trip instead
+// of the 72 dependent-free but scattered 8-byte loads per lane of features_from_epochs_kernel --
+// stages them in LDS, runs the filter bank (wave = 8 channels x 8 segments), normalises, and
+// writes the row back across the link.  C <= kSmallMaxC.
+constexpr int kSmallMaxC = 16;
+template <bool FAST>
+__global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
+                                                             int64_t n, int C, int nfeat,
+                                                             double* __restrict__ out) {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) double xs[kSmallMaxC * kWin];
+  __shared__ double feat[kSmallMaxC * 16];
+  __shared__ double norm;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t e = blockIdx.x;
+  const f64x2* src = (const f64x2*)(rows + e * C * kWin);
+  const int npairs = C * kWin / 2;  // <= 4096: at most 16 per thread
+  f64x2 v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int i = tid + 256 * k;
+    if (i < npairs) v[k] = src[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int i = tid + 256 * k;
+    if (i < npairs) *(f64x2*)(xs + 2 * i) = v[k];
+  }
+  __syncthreads();
+  const int F = C * nfeat;
+  const int s = lane & 7;
+  for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
+    const int c = c0 + (lane >> 3);
+    const bool valid = c < C;
+    const double* xr = xs + (valid ? c : 0) * kWin;
+    double x[kIn];
+#pragma unroll
+    for (int k = 0; k < kIn; ++k) x[k] = xr[(kSegLen * s + k) & (kWin - 1)];
+    double a6, d6;
+    dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
+    if (valid) {
+      if (s < nfeat) feat[c * nfeat + s] = a6;
+      if (8 + s < nfeat) feat[c * nfeat + 8 + s] = d6;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {  // SignalProcessing.normalize: Math.pow(f, 2) summed in index order
+    double acc = 0.0;
+    for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
+    norm = sqrt(acc);
+  }
+  __syncthreads();
+  for (int i = tid; i < F; i += 256) out[e * F + i] = feat[i] / norm;
+}
+
 // ---- synthetic recordings ------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -215,6 +272,21 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
   else
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<false>, grid, block, smem, st, ep, n, C,
                        skip, nfeat, row_stride, out);
+  return hipGetLastError();
+}
+
+bool features_small_supported(int C) { return C >= 1 && C <= dev::kSmallMaxC; }
+
+hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
+                                 bool fast, double* out) {
+  if (n == 0) return hipSuccess;
+  if (!features_small_supported(C)) return hipErrorNotSupported;
+  if (fast)
+    hipLaunchKernelGGL(dev::features_small_kernel<true>, dim3((unsigned)n), dim3(256), 0, st, rows,
+                       n, C, nfeat, out);
+  else
+    hipLaunchKernelGGL(dev::features_small_kernel<false>, dim3((unsigned)n), dim3(256), 0, st, rows,
+                       n, C, nfeat, out);
   return hipGetLastError();
 }
 

@@ -26,6 +26,11 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
 // epochs, 512 for the window-only rows the host path stages)
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
                                        int nfeat, bool fast, double* out, int row_stride = 750);
+// Small host batches (kernels.hip features_small_kernel): rows = n x C x 512 packed window rows,
+// one workgroup per epoch, C <= 16; rows / out may be device pointers of mapped pinned memory.
+bool features_small_supported(int C);
+hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
+                                 bool fast, double* out);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
 // Non-temporal reads pay when the regions neighbouring epochs read do not overlap: the average

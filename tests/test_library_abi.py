@@ -84,3 +84,12 @@ def test_plain_c_consumer(tmp_path):
     r = subprocess.run([exe, DOD01], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert "abi_consumer ok" in r.stdout
+
+
+def test_no_environment_knobs_in_the_product():
+    """The kernel choice of every call is a function of its arguments only: no getenv in the
+    library sources (the rejected perf-study variants live under tools/probes/rejected/)."""
+    csrc = os.path.join(REPO, "eeg_dataanalysispackage_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            assert "getenv(" not in open(os.path.join(csrc, f)).read(), f
