@@ -102,16 +102,28 @@ def traffic_from_profiles(workload_key):
     return best
 
 
-def valu_issue_from_profiles(applies):
-    """VALU issue share of window_kernel's cycles (SQ_INSTS_VALU x 4 / SIMD cycles at the
-    effective clock) from the committed counter pass; None for kernels it was not measured on."""
-    if not applies:
+CEILING_FILE = os.path.join("profiles", "r02_ceiling.json")
+
+
+def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
+    """The attainable bound of the dominant kernel (profiles/r02_ceiling.json): its VALU issue
+    time at the clock the chip holds under the kernel's own sustained power draw (SQ counters +
+    amd-smi under load), scaled to this launch's epochs, next to the live kernel time."""
+    if numerics != "fma":
         return None
+    key = {3: "window_kernel<int16,3> fma", 32: "window_c32_kernel fma"}.get(C)
     try:
-        d = json.load(open(os.path.join(REPO, "profiles", "r01k_pmc_window_fma.json")))
-        return d["derived"]["valu_issue_utilisation"]
+        k = json.load(open(os.path.join(REPO, CEILING_FILE)))["kernels"][key]
     except Exception:
         return None
+    ms = k["ceiling_ms"] * n / k["epochs_per_launch"]
+    return {"bound": "VALU issue at the power-capped clock (1.4 kW socket cap)",
+            "ms": round(ms, 4),
+            "frac": round(kernel_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_over_ceiling": round(ms / kernel_ms, 4),
+            "valu_instr_per_wave": k["valu_instr_per_wave"],
+            "clock_MHz_under_load": k["clock_MHz_under_load"],
+            "source": CEILING_FILE}
 
 
 def main():
@@ -237,7 +249,8 @@ def main():
         bpe = bytes_per_epoch(ct, C)
         path_gbs = n * bpe / (step_ms * 1e-3) / 1e9
         kernels = (["baseline_kernel<int16,3>", WINDOW_KERNEL] if C == 3 else
-                   ["baseline_any_kernel<int16>", "window_wide_kernel<int16>"])
+                   ["baseline_any_kernel<int16>",
+                    "window_c32_kernel" if C == 32 else "window_wide_kernel<int16>"])
         prof = traffic_from_profiles(workload_key)
         line = {
             "metric": METRIC,
@@ -283,10 +296,8 @@ def main():
                          "peak_TFs": FP64_VECTOR_PEAK_TFS,
                          "measured_fma_peak_TFs": FP64_FMA_MEASURED_TFS,
                          "frac": round(FLOP_PER_SIGNAL * C * n / (kernel_ms * 1e-3) / 1e12
-                                       / FP64_VECTOR_PEAK_TFS, 4),
-                         "valu_issue_utilisation": valu_issue_from_profiles(
-                             C == 3 and args.numerics == "fma"),
-                         "source": "profiles/r01k_pmc_window_fma.json (fma, c3)"},
+                                       / FP64_VECTOR_PEAK_TFS, 4)},
+                "ceiling": ceiling_from_profiles(C, args.numerics, n, kernel_ms, kernel_bytes),
             },
             "cpu_baseline": cpu,
         }

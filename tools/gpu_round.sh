@@ -38,6 +38,17 @@ for NUM in ${NUMS:-fma}; do
     --kernel window_kernel --workload-key "fused_dwt8_c3_int16_1000000_$NUM" \
     --algorithmic-bytes 3476000000 --out "$OUT/traffic_$NUM.json"
 done
+if [ "${C32TRAFFIC:-1}" = "1" ]; then  # configs[3]'s dominant kernel: trace + traffic passes
+  echo "== rocprofv3 kernel trace c32"; date
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c32" -o run -- python3 "$ROOT/bench.py" --workload c32 --cpu-sample 0 --alt-steps 0 > "$OUT/trace_c32.log" 2>&1 || { tail -30 "$OUT/trace_c32.log"; exit 1; }
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== pmc $C c32"; date
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex window_c32 --output-format csv -d "$OUT/pmc_${C}_c32" -o run -- python3 "$ROOT/bench.py" --workload c32 --steps 5 --warmup 1 --cpu-sample 0 --alt-steps 0 > "$OUT/pmc_${C}_c32.log" 2>&1 || { tail -30 "$OUT/pmc_${C}_c32.log"; exit 1; }
+  done
+  python3 "$ROOT/tools/traffic_summary.py" --fetch "$OUT/pmc_FETCH_SIZE_c32" --write "$OUT/pmc_WRITE_SIZE_c32" \
+    --kernel window_c32 --workload-key "fused_dwt8_c32_int16_250000_fma" \
+    --algorithmic-bytes 9250000000 --out "$OUT/traffic_c32_fma.json"
+fi
 cd "$ROOT"
 for WL in ${EXTRA:-c32 stream dropin big}; do
   echo "== bench $WL"; date
