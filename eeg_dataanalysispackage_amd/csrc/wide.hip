@@ -255,10 +255,10 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
 // configs[3]: the full 32-channel int16 montage with every channel through the DWT (512-dim rows),
 // one epoch per workgroup of 4 waves (wave w = channels 8w..8w+7, lane = (channel, segment)).
 // Everything the generic kernel computes from runtime sizes is constexpr here: the staging rows
-// (wave w issues rows w, w+4, ...; quad i = 257 sg + rem of the window lands at byte offset
-// 4096 sg + 16 rem, and the lane's (sg, rem) advance incrementally by 256 quads per row), the
-// signal -> channel map (shifts) and the row normalisation (FMA: rsqrt_nr, one multiply per
-// feature; EXACT keeps the reference's sequential sum and division).  Measured against the
+// (wave w issues rows w, w+4, ...; scalar row bases, two VALU instructions of lane offset per row,
+// no per-lane bounds test when the window lies inside the recording), the signal -> channel map
+// (shifts) and the row normalisation (FMA: rsqrt_nr, one multiply per feature; EXACT keeps the
+// reference's sequential sum and division).  Measured against the
 // generic kernel at FB = 64 (tools/probes, 666 launches of 250k epochs): 2.58 -> 2.46 ms,
 // 1,114 -> 1,040 VALU instructions per wave.
 template <bool FAST, bool STREAM>
@@ -280,30 +280,34 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   const int64_t Bq = B & ~(int64_t)15;
   constexpr int64_t span = (int64_t)64 * FB * 7 + 16 * SEGQ;
   const bool full = Bq >= 0 && Bq + span <= nbytes;
-  const uint8_t* sb = raw + Bq;
-  // row j = w + 4t, quad i = 64 j + lane = sg * SEGQ + rem
-  int i = 64 * w + lane;
-  int sg = i / SEGQ;
-  int rem = i - sg * SEGQ;
+  // Row j = w + 4t holds LDS quads i = 64 j + lane; quad i = SEGQ sg + rem lands from byte
+  // 4096 sg + 16 rem = 16 i - 16 sg of the window.  A row spans 64 < SEGQ quads, so it crosses at
+  // most one segment boundary: sg = s0 + [lane >= t_j] with s0 = floor(64 j / SEGQ), and the
+  // offset splits into a scalar row base (1024 j - 16 s0) and a per-lane 16 lane - 16 [lane >= t_j]
+  // (two VALU instructions per row).
+  const uint32_t lane16 = 16u * (uint32_t)lane;
 #pragma unroll
   for (int t = 0; t < (NROWS + 3) / 4; ++t) {
     const int j = w + 4 * t;
     if (j < NROWS) {  // uniform
-      const uint32_t off = (uint32_t)(64 * FB * sg + 16 * rem);
+      const int s0 = (64 * j) / SEGQ;
+      const int tj = SEGQ * (s0 + 1) - 64 * j;
+      const uint32_t voff = lane16 - (lane >= tj ? 16u : 0u);
+      const int64_t rowb = 1024 * (int64_t)j - 16 * (int64_t)s0;
       uint8_t* dst = win + (size_t)(64 * j) * 16;
-      if (64 * j + lane < EQ) {
-        if (full || (Bq + off >= 0 && Bq + off + 16 <= nbytes)) {
-          dma16_s<STREAM>(sb, off, dst);
+      const bool lane_in = 64 * j + 64 <= EQ || 64 * j + lane < EQ;
+      if (full) {  // uniform: the whole window lies inside the recording
+        if (lane_in) dma16_s<STREAM>(raw + Bq + rowb, voff, dst);
+      } else if (lane_in) {
+        const int64_t A = Bq + rowb + voff;
+        if (A >= 0 && A + 16 <= nbytes) {
+          dma16_s<STREAM>(raw + Bq + rowb, voff, dst);
         } else {
-          const wq_a4 v = wide_load16(raw, nbytes, Bq + off);
+          const wq_a4 v = wide_load16(raw, nbytes, A);
           uint32_t* d = (uint32_t*)(dst + 16 * lane);
           d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
       }
-      // next row: i += 256 (SEGQ = 257): the segment advances unless rem was 0
-      const bool adv = rem >= 1;
-      sg += adv ? 1 : 0;
-      rem = adv ? rem - 1 : 256;
     }
   }
   dma_drain();
