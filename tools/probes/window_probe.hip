@@ -37,7 +37,7 @@ int main() {
   double* out;
   (void)hipMalloc(&raw, nf * ct * 2);
   (void)hipMalloc(&pos, n * 8);
-  (void)hipMalloc(&base, n * ct * 4);
+  (void)hipMalloc(&base, eegfx::fused_scratch_bytes(n, ct));
   (void)hipMalloc(&out, n * 16 * ct * 8);
   (void)eegfx::launch_synth(0, raw, nf, ct, 0x5EED);
   std::vector<int64_t> hp(n);
