@@ -36,7 +36,7 @@ def bytes_per_epoch(ct, C):
     return 612 * ct * 2 + 8 + 16 * C * 8
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFS = 78.6                    # vendor fp64 vector spec (not in the guide)
-FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01b_perf_study.json)
+FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01/r01b_perf_study.json)
 FLOP_PER_SIGNAL = 2 * 5120                     # minimal a-path cascade, per channel
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED

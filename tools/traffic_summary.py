@@ -2,7 +2,7 @@
 """HBM traffic per launch of one kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
     python tools/traffic_summary.py --fetch DIR --write DIR --kernel window_kernel \
-        --workload-key fused_dwt8_c3_int16_1000000_fma --out profiles/r01_traffic_fma.json
+        --workload-key fused_dwt8_c3_int16_1000000_fma --out profiles/r02c_traffic_fma.json
 
 Corrections (MI355X_MICROARCH.md, "HBM"): both counters are in KiB; on gfx950 FETCH_SIZE reports
 half the bytes of a wide (16 B/lane) streaming read, so it is doubled; WRITE_SIZE is exact for
