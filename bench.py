@@ -82,6 +82,9 @@ def parse():
                     help="rehearsal only: 'gloo' runs the N>1 control flow without RCCL")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (a one-GPU box)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="rehearsal only: run the N>1 code path (process group, C-ABI gather) "
+                         "even with one rank")
     return ap.parse_args()
 
 
@@ -126,8 +129,27 @@ def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
             "source": CEILING_FILE}
 
 
+_JSON_OUT = None
+
+
+def emit(line):
+    """Prints the one JSON line on the process's original stdout (fd 1 at start-up)."""
+    out = _JSON_OUT or sys.stdout
+    print(json.dumps(line), file=out, flush=True)
+
+
+def _stdout_to_stderr():
+    """Everything else written to fd 1 -- RCCL's version banner at communicator creation, runtime
+    chatter -- goes to stderr, so stdout carries exactly the bench line."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main():
     args = parse()
+    _stdout_to_stderr()
     import torch
     import torch.distributed as dist
 
@@ -137,7 +159,7 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
-    distributed = world > 1
+    distributed = world > 1 or args.force_dist
     dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
     if distributed:
@@ -310,7 +332,7 @@ def main():
                 line["extract_plus_gather"] = {
                     "value": round(world * n / ((elapsed / args.steps) + gather["ms"] * 1e-3), 1),
                     "unit": "epochs/s", "gather_op": gather["op"]}
-        print(json.dumps(line), flush=True)
+        emit(line)
 
     ctx.close()
     if distributed:
@@ -455,7 +477,7 @@ def bench_dropin(args, rank, world, dev, dist):
     value = (native["single_epoch"]["epochs_per_s"] if native and "single_epoch" in native
              else 1.0 / med)
     if rank == 0:
-        print(json.dumps({
+        emit(({
             "metric": "per-call IFeatureExtraction latency through the C ABI (configs[0] drop-in)",
             "value": round(value, 1), "unit": "epochs/s per calling thread",
             "n_gpus": world, "steps": reps, "warmup": 20, "ms_per_step": round(med * 1e3, 4),
@@ -476,7 +498,7 @@ def bench_dropin(args, rank, world, dev, dist):
                              "sample": "the same epoch, oracle C restatement (full pyramid), "
                                        f"median of {reps} calls from C (Python: "
                                        f"{round(1.0 / med_cpu, 1)} epochs/s)"},
-        }), flush=True)
+        }))
 
 
 def bench_stream(args, rank, world, dev, dist):
@@ -540,7 +562,7 @@ def bench_stream(args, rank, world, dev, dist):
     del d_in, d_out
     if rank == 0:
         h2d = nf * 6 * args.steps / el / 1e9
-        print(json.dumps({
+        emit(({
             "metric": METRIC, "value": round(world * n * args.steps / el, 1), "unit": "epochs/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
@@ -556,7 +578,7 @@ def bench_stream(args, rank, world, dev, dist):
                           "note": "every frame crosses the host link once per step and every "
                                   "feature row once back; copy_only_ms = the same bytes moved by "
                                   "two concurrent plain copies (the bound), frac = that / step"},
-        }), flush=True)
+        }))
     ctx.close()
 
 
@@ -629,7 +651,7 @@ def bench_logreg(args, rank, world, dev, dist):
                          f"{cdt:.2f} s wall",
                "gpu_parity_on_sample": bool(np.linalg.norm(wg - wr) <= 1e-9 * np.linalg.norm(wr))}
     if rank == 0:
-        print(json.dumps({
+        emit(({
             "metric": f"{'SVM' if svm else 'logistic-regression'} SGD rows*iterations/s (MLlib "
                       f"{algo}, full batch) on the dwt-8 feature rows",
             "value": round(world * n * it * steps / elapsed, 1),
@@ -646,7 +668,7 @@ def bench_logreg(args, rank, world, dev, dist):
                          "traffic": None, "kernel": "lr_grad16_kernel + lr_update_kernel",
                          "bytes_per_iteration": bytes_iter,
                          "ms_per_iteration": round(per_iter * 1e3, 4)},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu}))
     ctx.close()
 
 
