@@ -269,23 +269,26 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
   wave_sync();
 }
 
-// Byte offset, from floor16(B_e), of the global quad that lands in LDS quad i of an epoch window
-// (segment i / SEGQ, quad i % SEGQ of that segment).  Depends on the lane only, so a kernel
-// computes it once per DMA row j (i = 64*j + lane) and every DMA of every epoch reuses it.
-template <int CT>
-__device__ __forceinline__ uint32_t quad_offset(int i) {
-  using G = Geometry<CT>;
-  const int sg = i / G::SEGQ;
-  return (uint32_t)(kSegLen * G::FB * sg + 16 * (i - G::SEGQ * sg));
-}
-
+// DMA rows of an epoch window: each row (one global_load_lds_dwordx4, lanes < SPR * SEGQ active)
+// carries SPR whole segments, so the lane's source offset is the same for every row:
+// lane l lands in segment SPR j + l / SEGQ, quad l % SEGQ, i.e. from byte
+// 64 FB (SPR j + l / SEGQ) + 16 (l % SEGQ) = (64 FB SPR) j + 16 l - (16 SEGQ - 64 FB) (l / SEGQ)
+// of floor16(B): a scalar row base plus one per-lane constant.
 template <int CT>
 struct DmaRows {
-  static constexpr int PER_E = (Geometry<CT>::EPQ + 63) / 64;  // 4 DMA rows per epoch window
-  uint32_t off[PER_E];
+  using G = Geometry<CT>;
+  static constexpr int SPR = 64 / G::SEGQ;                 // segments per row (2 for CT = 3)
+  static constexpr int PER_E = (8 + SPR - 1) / SPR;        // rows per epoch window (4)
+  static constexpr int LANES = SPR * G::SEGQ;              // active lanes per row (50)
+  static constexpr int ROWB = kSegLen * G::FB * SPR;       // source bytes per row (768)
+  static constexpr int ROWDW = G::SEGQ * SPR * 4;          // LDS dwords per row (200)
+  static_assert(SPR >= 1 && 8 % SPR == 0, "whole segments per row");
+  uint32_t off;
+  bool active;
   __device__ __forceinline__ explicit DmaRows(int lane) {
-#pragma unroll
-    for (int j = 0; j < PER_E; ++j) off[j] = quad_offset<CT>(64 * j + lane);
+    const int sg = lane / G::SEGQ;
+    off = (uint32_t)(16 * lane - (16 * G::SEGQ - kSegLen * G::FB) * sg);
+    active = lane < LANES;
   }
 };
 
@@ -317,15 +320,17 @@ __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64
     const uint8_t* sb = raw + Bq;
     uint32_t* dst = win + e * G::ESTR;
     if (((uint32_t)W[t] & 1u) == 0) {
+      if (rows.active) {
 #pragma unroll
-      for (int j = 0; j < PER_E; ++j)
-        if (64 * (j + 1) <= G::EPQ || 64 * j + lane < G::EPQ) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
-    } else {
+        for (int j = 0; j < PER_E; ++j)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
+      }
+    } else if (rows.active) {
 #pragma unroll
       for (int j = 0; j < PER_E; ++j) {
-        if (64 * j + lane >= G::EPQ) continue;
-        const int64_t A = Bq + rows.off[j];
-        if (A >= 0 && A + 16 <= nbytes) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
+        const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+        if (A >= 0 && A + 16 <= nbytes)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
         else need_fix = true;
       }
     }
@@ -346,9 +351,9 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
     const int64_t Bq = wb[e0 + e] & ~(int64_t)15;
 #pragma unroll
     for (int j = 0; j < PER_E; ++j) {
-      const int64_t A = Bq + rows.off[j];
-      if (64 * j + lane < G::EPQ && (A < 0 || A + 16 > nbytes))
-        lds_store4(win + e * G::ESTR + 256 * j + 4 * lane, load16(raw, nbytes, A));
+      const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+      if (rows.active && (A < 0 || A + 16 > nbytes))
+        lds_store4(win + e * G::ESTR + DmaRows<CT>::ROWDW * j + 4 * lane, load16(raw, nbytes, A));
     }
   }
 }
