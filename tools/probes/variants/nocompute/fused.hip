@@ -63,7 +63,15 @@ struct Geometry {
   static constexpr int ESTR = round_up_res(EPQ * 4, 32, 1);  // 801 dwords
   static constexpr int BASEQ = (kPre * FB + 15) / 16 + 1;    // 39 quads (600 B + misalignment)
   static constexpr int BSTR = round_up_res(BASEQ * 4, 32, 29);  // odd, 29 (mod 32)
+  // bytes a window DMA spans from floor16(B): 7 segments + the last segment's 25 quads
+  static constexpr int64_t SPANB = (int64_t)kSegLen * FB * 7 + 16 * (SEGQ - 1) + 16;
 };
+
+// Window word of an epoch, written by baseline_kernel for window_kernel: the byte offset of its
+// 512-frame window, B = (pos + 175) * FB (even), with bit 0 set when the DMA span from floor16(B)
+// does not lie wholly inside the recording (the guarded path).  The window kernel then needs no
+// 64-bit compares on its fast path (SALU has no 64-bit ordered compare on gfx950: every such
+// test was a VALU instruction pair per epoch).
 
 __device__ __forceinline__ void lds_store4(uint32_t* dst, const u32x4_a4& v) {
   dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
@@ -127,7 +135,7 @@ __device__ __forceinline__ void flag_position(int* err) {
 template <int CT, int C, int TILE, bool STREAM = false>
 __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
-    int64_t n, float* __restrict__ bout, int* __restrict__ err) {
+    int64_t n, float* __restrict__ bout, int64_t* __restrict__ wout, int* __restrict__ err) {
   using G = Geometry<CT>;
   constexpr int NT = (TILE * C + 63) / 64 * 64;
   __shared__ __attribute__((aligned(16))) uint32_t stage[TILE * G::BSTR];
@@ -139,7 +147,13 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   if (tid < TILE) {
     const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
     if (!position_ok(p, n_frames)) flag_position(err);
-    tB[tid] = (safe_position(p, n_frames) - kPre) * G::FB;
+    const int64_t sp = safe_position(p, n_frames);
+    tB[tid] = (sp - kPre) * G::FB;
+    if (tid < nt) {
+      const int64_t B = (sp + 175) * G::FB;
+      const int64_t Bq = B & ~(int64_t)15;
+      wout[t0 + tid] = B | ((Bq >= 0 && Bq + G::SPANB <= nbytes) ? 0 : 1);
+    }
   }
   __syncthreads();
   constexpr int ITERS = (TILE * G::BASEQ + NT - 1) / NT;
@@ -178,14 +192,6 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   if (e < nt) bout[(t0 + e) * C + c] = b / (float)kPre;
 }
 
-// Byte offset of sub-tile epoch e's window: B_e = (pos + 175) * FB; quads are fetched from
-// floor16(B_e) and the lanes fold (B_e & 15) into their read base.  e0 and e are wave-uniform,
-// so these are scalar loads (lgkmcnt), which keeps every vector-memory counter slot for the DMAs.
-template <int CT>
-__device__ __forceinline__ int64_t window_byte(const int64_t* __restrict__ pos, int64_t e,
-                                               int64_t n_frames) {
-  return (safe_position(pos[e], n_frames) + 175) * (2 * CT);
-}
 
 // a3 + a6 + a7 fused into level 1 (dwt8.h level1_jit): (double)((float)raw * res - b), the
 // multiply and the subtraction each one correctly rounded fp32 operation
@@ -263,63 +269,68 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
   wave_sync();
 }
 
-// Byte offset, from floor16(B_e), of the global quad that lands in LDS quad i of an epoch window
-// (segment i / SEGQ, quad i % SEGQ of that segment).  Depends on the lane only, so a kernel
-// computes it once per DMA row j (i = 64*j + lane) and every DMA of every epoch reuses it.
-template <int CT>
-__device__ __forceinline__ uint32_t quad_offset(int i) {
-  using G = Geometry<CT>;
-  const int sg = i / G::SEGQ;
-  return (uint32_t)(kSegLen * G::FB * sg + 16 * (i - G::SEGQ * sg));
-}
-
+// DMA rows of an epoch window: each row (one global_load_lds_dwordx4, lanes < SPR * SEGQ active)
+// carries SPR whole segments, so the lane's source offset is the same for every row:
+// lane l lands in segment SPR j + l / SEGQ, quad l % SEGQ, i.e. from byte
+// 64 FB (SPR j + l / SEGQ) + 16 (l % SEGQ) = (64 FB SPR) j + 16 l - (16 SEGQ - 64 FB) (l / SEGQ)
+// of floor16(B): a scalar row base plus one per-lane constant.
 template <int CT>
 struct DmaRows {
-  static constexpr int PER_E = (Geometry<CT>::EPQ + 63) / 64;  // 4 DMA rows per epoch window
-  uint32_t off[PER_E];
+  using G = Geometry<CT>;
+  static constexpr int SPR = 64 / G::SEGQ;                 // segments per row (2 for CT = 3)
+  static constexpr int PER_E = (8 + SPR - 1) / SPR;        // rows per epoch window (4)
+  static constexpr int LANES = SPR * G::SEGQ;              // active lanes per row (50)
+  static constexpr int ROWB = kSegLen * G::FB * SPR;       // source bytes per row (768)
+  static constexpr int ROWDW = G::SEGQ * SPR * 4;          // LDS dwords per row (200)
+  static_assert(SPR >= 1 && 8 % SPR == 0, "whole segments per row");
+  uint32_t off;
+  bool active;
   __device__ __forceinline__ explicit DmaRows(int lane) {
-#pragma unroll
-    for (int j = 0; j < PER_E; ++j) off[j] = quad_offset<CT>(64 * j + lane);
+    const int sg = lane / G::SEGQ;
+    off = (uint32_t)(16 * lane - (16 * G::SEGQ - kSegLen * G::FB) * sg);
+    active = lane < LANES;
   }
 };
 
 // Issues the LDS-DMA of one sub-tile's windows: wave w stages epochs w, w+C, w+2C, ... (every
-// DMA row of each).  The marker positions of those epochs are loaded (scalar) before the first
-// DMA, so the DMAs leave back to back; an epoch whose whole window lies inside the recording (a
-// scalar test) takes the unguarded path.  Returns whether some quad of this lane could not be
-// DMA'd (the window reaches past either end of the recording).
+// DMA row of each).  The window words of those epochs are loaded (scalar: e0 and e are
+// wave-uniform, so these are lgkmcnt loads and every vector-memory counter slot stays with the
+// DMAs) before the first DMA, so the DMAs leave back to back; an epoch whose window lies wholly
+// inside the recording (bit 0 of its word clear) takes the unguarded path.  Returns whether some
+// quad of this lane could not be DMA'd (the window reaches past either end of the recording).
 template <int CT, int C, bool NT>
 __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
-                                          const int64_t* __restrict__ pos, int64_t n, int64_t e0,
+                                          const int64_t* __restrict__ wb, int64_t e0, int ne,
                                           uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
   constexpr int PER_E = DmaRows<CT>::PER_E;
   constexpr int NE = (kSub + C - 1) / C;
-  constexpr int64_t kSpanB = kSegLen * G::FB * 7 + 16 * (G::SEGQ - 1) + 16;
-  const int64_t n_frames = nbytes / G::FB;
-  int64_t Bq[NE];
+  int64_t W[NE];
 #pragma unroll
   for (int t = 0; t < NE; ++t) {  // unconditional (clamped) loads: one scalar round trip
-    const int64_t ei = e0 + (w + t * C < kSub ? w + t * C : kSub - 1);
-    Bq[t] = window_byte<CT>(pos, ei < n ? ei : n - 1, n_frames) & ~(int64_t)15;
+    const int e = w + t * C < kSub ? w + t * C : kSub - 1;
+    W[t] = wb[e0 + (e < ne ? e : ne - 1)];
   }
   bool need_fix = false;
 #pragma unroll
   for (int t = 0; t < NE; ++t) {
     const int e = w + t * C;
-    if (e >= kSub || e0 + e >= n) continue;  // uniform
-    const uint8_t* sb = raw + Bq[t];
+    if (e >= kSub || e >= ne) continue;  // uniform
+    const int64_t Bq = W[t] & ~(int64_t)15;
+    const uint8_t* sb = raw + Bq;
     uint32_t* dst = win + e * G::ESTR;
-    if (Bq[t] >= 0 && Bq[t] + kSpanB <= nbytes) {
+    if (((uint32_t)W[t] & 1u) == 0) {
+      if (rows.active) {
 #pragma unroll
-      for (int j = 0; j < PER_E; ++j)
-        if (64 * (j + 1) <= G::EPQ || 64 * j + lane < G::EPQ) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
-    } else {
+        for (int j = 0; j < PER_E; ++j)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
+      }
+    } else if (rows.active) {
 #pragma unroll
       for (int j = 0; j < PER_E; ++j) {
-        if (64 * j + lane >= G::EPQ) continue;
-        const int64_t A = Bq[t] + rows.off[j];
-        if (A >= 0 && A + 16 <= nbytes) dma16_s<NT>(sb, rows.off[j], dst + 256 * j);
+        const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+        if (A >= 0 && A + 16 <= nbytes)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
         else need_fix = true;
       }
     }
@@ -331,19 +342,18 @@ __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64
 // partial quads at either end of the recording.
 template <int CT, int C>
 __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64_t nbytes,
-                                          const int64_t* __restrict__ pos, int64_t n, int64_t e0,
+                                          const int64_t* __restrict__ wb, int64_t e0, int ne,
                                           uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
   constexpr int PER_E = DmaRows<CT>::PER_E;
-  const int64_t n_frames = nbytes / G::FB;
   for (int e = w; e < kSub; e += C) {
-    if (e0 + e >= n) break;
-    const int64_t Bq = window_byte<CT>(pos, e0 + e, n_frames) & ~(int64_t)15;
+    if (e >= ne) break;
+    const int64_t Bq = wb[e0 + e] & ~(int64_t)15;
 #pragma unroll
     for (int j = 0; j < PER_E; ++j) {
-      const int64_t A = Bq + rows.off[j];
-      if (64 * j + lane < G::EPQ && (A < 0 || A + 16 > nbytes))
-        lds_store4(win + e * G::ESTR + 256 * j + 4 * lane, load16(raw, nbytes, A));
+      const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+      if (rows.active && (A < 0 || A + 16 > nbytes))
+        lds_store4(win + e * G::ESTR + DmaRows<CT>::ROWDW * j + 4 * lane, load16(raw, nbytes, A));
     }
   }
 }
@@ -356,13 +366,12 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 // 18 waves per CU), and one wave normalises and stores the 8 rows.
 template <int CT, int C, bool FAST, bool NT>
 __global__ __launch_bounds__(64 * C, 4) void window_kernel(
-    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
     const float* __restrict__ base, int64_t n, double* __restrict__ out) {
   using G = Geometry<CT>;
   constexpr int F = C * 16;
   static_assert(kSub * F * 8 <= kSub * G::ESTR * 4, "feature rows alias the window buffer");
   __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
-  __shared__ int tdelta[kSub];
   __shared__ double norm[kSub];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -371,18 +380,20 @@ __global__ __launch_bounds__(64 * C, 4) void window_kernel(
   const int col = sel.col[w];
   const float r = sel.res[w];
   const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * kSub;
+  const int64_t rest = n - e0;  // >= 1
+  const int ne = (rest >> 31) != 0 ? kSub : ((int)rest < kSub ? (int)rest : kSub);
 
-  if (w == 0 && lane < kSub)
-    tdelta[lane] = e0 + lane < n ? (int)(window_byte<CT>(pos, e0 + lane, n_frames) & 15) : 0;
-  const float b = (e0 + el < n) ? base[(e0 + el) * C + w] : 0.0f;
+  const bool mine = el < ne;
+  const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
+  const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
   const DmaRows<CT> rows(lane);
-  if (dma_issue<CT, C, NT>(raw, nbytes, pos, n, e0, win, w, lane, rows))
-    dma_fixup<CT, C>(raw, nbytes, pos, n, e0, win, w, lane, rows);
+  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
   dma_drain();
   __syncthreads();
 
   // this lane's 64 samples + 8 halo samples of signal (epoch el, channel w), decoded in level 1
-  const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + tdelta[el] + 2 * col;
+  const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col;
   const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
   const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
   // ABLATION (tools/probes only): no decode and no filter bank; two samples keep the window live
@@ -398,7 +409,7 @@ __global__ __launch_bounds__(64 * C, 4) void window_kernel(
   fb[slot] = a6;
   fb[slot + 8] = d6;
   __syncthreads();
-  if (w == 0) normalise_store<F, FAST>(fb, norm, out + e0 * F, (n - e0) < kSub ? (int)(n - e0) : kSub, lane);
+  if (w == 0) normalise_store<F, FAST>(fb, norm, out + e0 * F, ne, lane);
 }
 
 }  // namespace dev
@@ -415,7 +426,14 @@ bool fused_supported(int fmt, int ct, int C, const double* out) {
   return fmt == 0 && ct == 3 && C == 3 && ((uintptr_t)out & 15) == 0;
 }
 
-size_t fused_scratch_bytes(int64_t n, int C) { return sizeof(float) * (size_t)n * (size_t)C; }
+// Scratch of the fused path: [n][C] float baselines, then (16-byte aligned) the n int64 window
+// words of baseline_kernel.
+static size_t window_words_offset(int64_t n, int C) {
+  return (sizeof(float) * (size_t)n * (size_t)C + 15) & ~(size_t)15;
+}
+size_t fused_scratch_bytes(int64_t n, int C) {
+  return window_words_offset(n, C) + sizeof(int64_t) * (size_t)n;
+}
 
 int64_t fused_window_bytes_per_epoch(int ct, int C) {
   // window + 12 B of baselines + position + feature row
@@ -430,12 +448,13 @@ hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_fram
   // 64 epochs per workgroup; 16/32/128 measured the same or slower.  Streaming
   // reads unless another epoch's window or baseline may share the pre-stimulus frames.
   const dim3 g((unsigned)((n + 63) / 64));
+  int64_t* words = (int64_t*)((uint8_t*)scratch + window_words_offset(n, C));
   if (streaming_reads(n_frames, n, dev::kPre + 687))
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,
-                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, err);
+                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, words, err);
   else
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,
-                       n_frames, sel, pos, n, (float*)scratch, err);
+                       n_frames, sel, pos, n, (float*)scratch, words, err);
   return hipGetLastError();
 }
 
@@ -445,11 +464,13 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
   const float* bs = (const float*)scratch;
+  const int64_t* words = (const int64_t*)((const uint8_t*)scratch + window_words_offset(n, C));
+  (void)pos;  // read by launch_fused_baseline, which wrote the window words
   const dim3 g((unsigned)((n + dev::kSub - 1) / dev::kSub));
   const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
 #define EEGFX_WIN(FA, NTV)                                                                         \
   hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192), 0, st, (const uint8_t*)raw, \
-                     n_frames, sel, pos, bs, n, out)
+                     n_frames, sel, words, bs, n, out)
   if (fast) { if (nt) EEGFX_WIN(true, true); else EEGFX_WIN(true, false); }
   else { if (nt) EEGFX_WIN(false, true); else EEGFX_WIN(false, false); }
 #undef EEGFX_WIN
