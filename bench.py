@@ -497,7 +497,8 @@ def bench_dropin(args, rank, world, dev, dist):
                              "unit": "epochs/s per thread", "cores": 1, "kind": "port",
                              "sample": "the same epoch, oracle C restatement (full pyramid), "
                                        f"median of {reps} calls from C (Python: "
-                                       f"{round(1.0 / med_cpu, 1)} epochs/s)"},
+                                       f"{round(1.0 / med_cpu, 1)} epochs/s)",
+                             "optimised": (native or {}).get("cpu_optimised_single_thread")},
         }))
 
 
@@ -674,33 +675,62 @@ def bench_logreg(args, rank, world, dev, dist):
 
 def cpu_baseline(args, raw, gpu_out, ct, C):
     """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
-    threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload."""
+    threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload.
+
+    SURVEY.md 8(d): the reference-faithful variant is `value`; beside it the optimised CPU
+    restatement (oracle.process_recording_fast: minimal cascade over only the 612 frames that reach
+    the features, 4 epochs per AVX2 vector, bit-identical features), and both at one thread on a
+    smaller sample.  Every leg is the median of 5 timed runs after a warm-up."""
     from oracle import oracle
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10, args.epochs)
+    k1 = max(1, min(k // 25, 20000 if C == 3 else 2000))  # one-thread sample
     host = raw[: FRAMES_PER_EPOCH * k + 2000].cpu().numpy()
     pos = np.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (k + 1), FRAMES_PER_EPOCH, dtype=np.int64)
     cols = list(range(C))
-    oracle.process_recording(host[: FRAMES_PER_EPOCH * 200 + 2000], cols, [0.1] * C,
-                             pos[:200], faithful=True, nthreads=threads)  # warm-up
-    t0 = time.perf_counter()
-    feats = oracle.process_recording(host, cols, [0.1] * C, pos, faithful=True,
-                                     nthreads=threads)
-    dt = time.perf_counter() - t0
+
+    def run(h, p, faithful, nthreads):
+        if faithful:
+            return oracle.process_recording(h, cols, [0.1] * C, p, faithful=True,
+                                            nthreads=nthreads)
+        return oracle.process_recording_fast(h, cols, [0.1] * C, p, nthreads=nthreads)
+
+    def leg(n, faithful, nthreads, reps=5):
+        h = host[: FRAMES_PER_EPOCH * n + 2000]
+        run(h[: FRAMES_PER_EPOCH * 200 + 2000], pos[: min(200, n)], faithful, nthreads)
+        times, feats = [], None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            feats = run(h, pos[:n], faithful, nthreads)
+            times.append(time.perf_counter() - t0)
+        dt = float(np.median(times))
+        return n / dt, dt, feats
+
+    value, dt, feats = leg(k, True, threads)
     gpu = gpu_out[:k].cpu().numpy()
     if args.numerics == "exact":
         parity = bool(np.array_equal(gpu, feats, equal_nan=True))
     else:
         parity = bool(np.max(np.abs(gpu - feats)) <= 1e-9)
+    faithful_1, _, _ = leg(k1, True, 1)
+    minimal_n, _, feats_min = leg(k, False, threads)
+    minimal_1, _, _ = leg(k1, False, 1)
     return {
-        "value": round(k / dt, 1),
+        "value": round(value, 1),
         "unit": "epochs/s",
         "cores": threads,
         "kind": "port",
         "sample": f"first {k} epochs of the rank-0 synthetic recording, C restatement of the "
                   f"Java path (full 6-level pyramid), {threads} threads over contiguous ranges, "
-                  f"{dt:.2f} s wall",
+                  f"median of 5 runs of {dt:.2f} s wall",
         "gpu_parity_on_sample": parity,
+        "variants": {
+            "faithful_1_thread": {"value": round(faithful_1, 1), "sample_epochs": k1},
+            "optimised": {"value": round(minimal_n, 1), "cores": threads, "sample_epochs": k,
+                                "bit_identical_to_faithful": bool(np.array_equal(
+                                    feats, feats_min, equal_nan=True))},
+            "optimised_1_thread": {"value": round(minimal_1, 1), "sample_epochs": k1},
+        },
     }
 
 

@@ -5,7 +5,7 @@
  * `cpu_baseline` leg of bench.py.  Nothing in the product path
  * (eeg_dataanalysispackage_amd/, include/) links, loads or calls it.
  *
- * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off, no fast-math, so every
+ * Build: oracle/Makefile  (gcc -O3 -ffp-contract=off, no fast-math, so every
  * double/float operation below is one correctly rounded IEEE op in source order).
  *
  * What it restates (all paths relative to the reference checkout):
@@ -210,4 +210,183 @@ void oracle_process_recording(const void* raw, int fmt, int64_t n_frames, int ct
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   free(th);
   free(jobs);
+}
+
+/* ------------------------------------------ optimised CPU baseline (bench only)
+ *
+ * The same operations as process_range(faithful = 0) in the same order for every epoch, so its
+ * features are bit-identical to the faithful path (the unused detail bands never feed back), but
+ * organised for a CPU: only the 612 frames that reach the features are decoded (100 baseline +
+ * the 512-sample window), the periodic cascade runs on a buffer extended by 8 samples instead of a
+ * modulo per tap, nothing is allocated per epoch, and VE epochs advance together with the epoch
+ * index innermost so the compiler vectorises across epochs (an AVX2 clone is picked at run time).
+ * Used only by bench.py's cpu_baseline leg and the tests that pin it to the faithful path. */
+#define VE 4
+#define FAST_WIN 512
+#define FAST_EXT 8 /* 2i + j <= n + 7 for the last output of a level */
+
+typedef double v4d __attribute__((vector_size(VE * sizeof(double))));
+
+/* unaligned vector load / store (macros: a vector-returning helper trips -Wpsabi) */
+#define LD4(dst, p) memcpy(&(dst), (p), sizeof(v4d))
+#define ST4(p, v) memcpy((p), &(v), sizeof(v4d))
+
+/* x: [n + 8][VE] samples (epoch innermost), t: scratch of the same size; coef: [16][VE]. */
+__attribute__((target_clones("avx2", "default")))
+static void fast_cascade(double* x, double* t, int nfeat, double* coef) {
+  int n = FAST_WIN;
+  while (n / 2 >= TAPS) {
+    const int h = n / 2;
+    memcpy(x + (size_t)n * VE, x, sizeof(double) * FAST_EXT * VE);
+    for (int i = 0; i < h; ++i) {
+      v4d a = {0.0, 0.0, 0.0, 0.0};
+      for (int j = 0; j < TAPS; ++j) {
+        v4d v;
+        LD4(v, x + (size_t)(2 * i + j) * VE);
+        a += v * H[j];
+      }
+      ST4(t + (size_t)i * VE, a);
+    }
+    double* s = x;
+    x = t;
+    t = s;
+    n = h;
+  }
+  /* last level (n = 16): approximations and details */
+  const int h = n / 2;
+  memcpy(x + (size_t)n * VE, x, sizeof(double) * FAST_EXT * VE);
+  for (int i = 0; i < h; ++i) {
+    v4d a = {0.0, 0.0, 0.0, 0.0}, d = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < TAPS; ++j) {
+      v4d v;
+      LD4(v, x + (size_t)(2 * i + j) * VE);
+      a += v * H[j];
+      d += v * G[j];
+    }
+    if (i < nfeat) ST4(coef + (size_t)i * VE, a);
+    if (i + h < nfeat) ST4(coef + (size_t)(i + h) * VE, d);
+  }
+}
+
+static void fast_range(const void* raw, int fmt, int64_t n_frames, int ct, const int32_t* cols,
+                       const float* res, int C, const int64_t* pos, int64_t e0, int64_t e1,
+                       int skip, int nfeat, double* feat) {
+  double* xb = (double*)malloc(sizeof(double) * (size_t)(FAST_WIN + FAST_EXT) * VE * 2);
+  double* tb = xb + (size_t)(FAST_WIN + FAST_EXT) * VE;
+  double coef[16 * VE];
+  for (int64_t g = e0; g < e1; g += VE) {
+    const int ne = (int)((e1 - g) < VE ? (e1 - g) : VE);
+    for (int c = 0; c < C; ++c) {
+      for (int e = 0; e < VE; ++e) {
+        if (e >= ne) {
+          for (int j = 0; j < FAST_WIN; ++j) xb[(size_t)j * VE + e] = 0.0;
+          continue;
+        }
+        const int64_t lo = pos[g + e] - PRE;
+        const int64_t w0 = lo + PRE + skip;
+        const float r = res[c];
+        float b = 0.0f;
+        if (w0 + FAST_WIN <= n_frames && fmt == 0) { /* the whole cut is inside the recording */
+          const int16_t* p = (const int16_t*)raw + lo * ct + cols[c];
+          for (int i = 0; i < PRE; ++i) b += (float)p[(size_t)i * ct] * r;
+          b = b / (float)PRE;
+          const int16_t* q = (const int16_t*)raw + w0 * ct + cols[c];
+          for (int j = 0; j < FAST_WIN; ++j)
+            xb[(size_t)j * VE + e] = (double)((float)q[(size_t)j * ct] * r - b);
+          continue;
+        }
+        for (int i = 0; i < PRE; ++i) {
+          const int64_t f = lo + i;
+          b += (f < n_frames) ? decode_sample(raw, fmt, f, ct, cols[c], r) : 0.0f;
+        }
+        b = b / (float)PRE;
+        for (int j = 0; j < FAST_WIN; ++j) {
+          const int64_t f = w0 + j;
+          const float v = (f < n_frames) ? decode_sample(raw, fmt, f, ct, cols[c], r) : 0.0f;
+          xb[(size_t)j * VE + e] = (double)(v - b);
+        }
+      }
+      fast_cascade(xb, tb, nfeat, coef);
+      for (int e = 0; e < ne; ++e)
+        for (int j = 0; j < nfeat; ++j)
+          feat[(size_t)(g + e) * C * nfeat + (size_t)c * nfeat + j] = coef[(size_t)j * VE + e];
+    }
+    for (int e = 0; e < ne; ++e) {
+      double* f = feat + (size_t)(g + e) * C * nfeat;
+      double s = 0.0;
+      for (int i = 0; i < C * nfeat; ++i) s += f[i] * f[i];
+      s = sqrt(s);
+      for (int i = 0; i < C * nfeat; ++i) f[i] = f[i] / s;
+    }
+  }
+  free(xb);
+}
+
+typedef struct {
+  const void* raw; int fmt; int64_t n_frames; int ct; const int32_t* cols; const float* res;
+  int C; const int64_t* pos; int64_t e0, e1; int skip, nfeat; double* feat;
+} fast_job_t;
+
+static void* fast_job_main(void* p) {
+  fast_job_t* j = (fast_job_t*)p;
+  fast_range(j->raw, j->fmt, j->n_frames, j->ct, j->cols, j->res, j->C, j->pos, j->e0, j->e1,
+             j->skip, j->nfeat, j->feat);
+  return NULL;
+}
+
+/* Returns 0, or -1 when the parameters are outside the optimised layout (win 512, nfeat <= 16,
+ * skip + 512 <= 750): callers then use oracle_process_recording. */
+int oracle_process_recording_fast(const void* raw, int fmt, int64_t n_frames, int ct,
+                                  const int32_t* cols, const float* res, int C,
+                                  const int64_t* pos, int64_t n_epochs, int skip, int win,
+                                  int nfeat, int nthreads, double* feat) {
+  if (win != FAST_WIN || nfeat < 1 || nfeat > 16 || skip < 0 || skip + win > POST) return -1;
+  init_g();
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  fast_job_t* jobs = (fast_job_t*)malloc(sizeof(fast_job_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; ++t) {
+    /* ranges start on VE boundaries so every group but the last is full */
+    const int64_t groups = (n_epochs + VE - 1) / VE;
+    const int64_t a = groups * t / nthreads * VE, b = groups * (t + 1) / nthreads * VE;
+    fast_job_t j = {raw, fmt, n_frames, ct, cols, res, C, pos, a, b < n_epochs ? b : n_epochs,
+                    skip, nfeat, feat};
+    jobs[t] = j;
+    pthread_create(&th[t], NULL, fast_job_main, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}
+
+/* The optimised CPU form of WaveletTransform.extractFeatures on caller epochs (double[n][C][750]):
+ * the channels of one epoch share the vector lanes (groups of VE), so a single-epoch call -- the
+ * per-epoch drop-in of SURVEY.md 8b -- is vectorised too.  Bit-identical to
+ * oracle_extract_features.  Returns -1 outside the optimised layout (see above). */
+int oracle_extract_features_fast(const double* epochs, int64_t n, int C, int skip, int win,
+                                 int nfeat, double* out) {
+  if (win != FAST_WIN || nfeat < 1 || nfeat > 16 || skip < 0 || skip + win > POST) return -1;
+  init_g();
+  double* xb = (double*)malloc(sizeof(double) * (size_t)(FAST_WIN + FAST_EXT) * VE * 2);
+  double* tb = xb + (size_t)(FAST_WIN + FAST_EXT) * VE;
+  double coef[16 * VE];
+  for (int64_t e = 0; e < n; ++e) {
+    const double* ep = epochs + (size_t)e * C * POST;
+    double* f = out + (size_t)e * C * nfeat;
+    for (int c0 = 0; c0 < C; c0 += VE) {
+      for (int j = 0; j < FAST_WIN; ++j)
+        for (int l = 0; l < VE; ++l)
+          xb[(size_t)j * VE + l] = (c0 + l < C) ? ep[(size_t)(c0 + l) * POST + skip + j] : 0.0;
+      fast_cascade(xb, tb, nfeat, coef);
+      for (int l = 0; l < VE && c0 + l < C; ++l)
+        for (int j = 0; j < nfeat; ++j) f[(c0 + l) * nfeat + j] = coef[(size_t)j * VE + l];
+    }
+    double s = 0.0;
+    for (int i = 0; i < C * nfeat; ++i) s += f[i] * f[i];
+    s = sqrt(s);
+    for (int i = 0; i < C * nfeat; ++i) f[i] = f[i] / s;
+  }
+  free(xb);
+  return 0;
 }

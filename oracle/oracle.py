@@ -48,6 +48,13 @@ def lib() -> ctypes.CDLL:
         L.oracle_process_recording.argtypes = [c_void_p, c_int, c_int64, c_int, c_void_p, c_void_p,
                                                c_int, c_void_p, c_int64, c_int, c_int, c_int, c_int,
                                                c_int, c_void_p]
+        L.oracle_process_recording_fast.argtypes = [c_void_p, c_int, c_int64, c_int, c_void_p,
+                                                    c_void_p, c_int, c_void_p, c_int64, c_int,
+                                                    c_int, c_int, c_int, c_void_p]
+        L.oracle_process_recording_fast.restype = c_int
+        L.oracle_extract_features_fast.argtypes = [c_void_p, c_int64, c_int, c_int, c_int, c_int,
+                                                   c_void_p]
+        L.oracle_extract_features_fast.restype = c_int
         for f in (L.oracle_decode_epochs, L.oracle_extract_features, L.oracle_process_recording):
             f.restype = None
         _lib = L
@@ -84,6 +91,17 @@ def extract_features(epochs: np.ndarray, skip=175, win=512, nfeat=16,
     return out
 
 
+def extract_features_fast(epochs: np.ndarray, skip=175, win=512, nfeat=16) -> np.ndarray:
+    """The optimised CPU extractFeatures (channels share the vector lanes); bit-identical to
+    extract_features.  The per-thread CPU rate beside the drop-in (bench.py --workload dropin)."""
+    ep = np.ascontiguousarray(epochs, dtype=np.float64)
+    n, C, _ = ep.shape
+    out = np.empty((n, C * nfeat), dtype=np.float64)
+    if lib().oracle_extract_features_fast(_p(ep), n, C, skip, win, nfeat, _p(out)) != 0:
+        raise ValueError("extract_features_fast: win must be 512, nfeat <= 16, skip + win <= 750")
+    return out
+
+
 def process_recording(raw: np.ndarray, cols, res, pos, faithful=True, nthreads=1,
                       skip=175, win=512, nfeat=16) -> np.ndarray:
     raw = np.ascontiguousarray(raw)
@@ -96,6 +114,26 @@ def process_recording(raw: np.ndarray, cols, res, pos, faithful=True, nthreads=1
     lib().oracle_process_recording(_p(raw), fmt, n_frames, ct, _p(cols_a), _p(res_a),
                                    len(cols_a), _p(pos_a), len(pos_a), skip, win, nfeat,
                                    1 if faithful else 0, nthreads, _p(out))
+    return out
+
+
+def process_recording_fast(raw: np.ndarray, cols, res, pos, nthreads=1, skip=175, win=512,
+                           nfeat=16) -> np.ndarray:
+    """The optimised CPU baseline: minimal cascade over only the frames that reach
+    the features, epochs vectorised in groups; bit-identical to process_recording (bench.py's
+    cpu_baseline leg; tests/test_oracle_golden.py pins it)."""
+    raw = np.ascontiguousarray(raw)
+    fmt = 0 if raw.dtype == np.int16 else 1
+    n_frames, ct = raw.shape
+    cols_a = np.ascontiguousarray(cols, dtype=np.int32)
+    res_a = np.ascontiguousarray(res, dtype=np.float32)
+    pos_a = np.ascontiguousarray(pos, dtype=np.int64)
+    out = np.empty((len(pos_a), len(cols_a) * nfeat), dtype=np.float64)
+    rc = lib().oracle_process_recording_fast(_p(raw), fmt, n_frames, ct, _p(cols_a), _p(res_a),
+                                             len(cols_a), _p(pos_a), len(pos_a), skip, win, nfeat,
+                                             nthreads, _p(out))
+    if rc != 0:
+        raise ValueError("process_recording_fast: win must be 512, nfeat <= 16, skip + win <= 750")
     return out
 
 

@@ -105,3 +105,45 @@ def test_zero_padded_epoch_past_end():
     assert np.all(ep[1] == 0.0)  # pos-100 == len: all-zero epoch (baseline 0)
     f = oracle.extract_features(ep[1:])
     assert np.all(np.isnan(f))   # 0/0 in SignalProcessing.normalize
+
+
+def test_optimised_cpu_baseline_bit_identical(info_train):
+    # bench.py's optimised CPU leg must compute the same features bit for bit:
+    # the reference recording, then ragged / zero-padded tails, other layouts, float32 data.
+    raw = np.fromfile(DOD02.replace("DoD_2015_02", "DoD2015_01") + ".eeg", dtype="<i2").reshape(-1, 3)
+    for nt in (1, 3):
+        fast = oracle.process_recording_fast(raw, [0, 1, 2], [0.1] * 3, info_train[2], nthreads=nt)
+        assert oracle.java_feature_sum(fast) == FEATURE_SUM_GOLDEN
+        assert np.array_equal(fast.view(np.int64),
+                              oracle.extract_features(info_train[0]).view(np.int64))
+    rng = np.random.default_rng(7)
+    for ct, cols, f32 in ((3, [0, 1, 2], False), (5, [4, 0, 2], False), (4, [1, 3], True)):
+        k = 37
+        raw = (rng.integers(-3000, 3000, size=(1000 * k + 500, ct)) - 20000).astype(np.int16)
+        if f32:
+            raw = (rng.standard_normal((1000 * k + 500, ct)) * 100).astype(np.float32)
+        pos = np.arange(1000, 1000 * (k + 1), 1000, dtype=np.int64)
+        pos[-1] = raw.shape[0] + 100      # pos - 100 == n_frames: all-zero epoch -> NaN row
+        pos[-2] = raw.shape[0] - 300      # window runs past the end: zero padding
+        res = [0.1, 0.25, 0.5][: len(cols)]
+        want = oracle.process_recording(raw, cols, res, pos, faithful=True)
+        for nt in (1, 4, 64):
+            got = oracle.process_recording_fast(raw, cols, res, pos, nthreads=nt)
+            assert np.array_equal(got.view(np.int64), want.view(np.int64)), (ct, nt)
+    with pytest.raises(ValueError):
+        oracle.process_recording_fast(raw, cols, res, pos, win=256)
+
+
+def test_optimised_extract_features_bit_identical(info_train):
+    ep = info_train[0]
+    want = oracle.extract_features(ep)
+    for i in range(len(ep)):  # one epoch per call, as the drop-in calls it
+        got = oracle.extract_features_fast(ep[i:i + 1])
+        assert np.array_equal(got.view(np.int64), want[i:i + 1].view(np.int64))
+    rng = np.random.default_rng(11)
+    for C in (1, 4, 5, 9):
+        e = rng.standard_normal((6, C, 750)) * 30
+        e[2] = 0.0  # all-zero epoch: NaN row like SignalProcessing.normalize
+        a = oracle.extract_features(e)
+        b = oracle.extract_features_fast(e)
+        assert np.array_equal(a.view(np.int64), b.view(np.int64)), C

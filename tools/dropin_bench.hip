@@ -10,7 +10,8 @@
 //   threads  T threads, one context each (include/eegfx.h's rule for Spark executor threads),
 //            all calling concurrently;
 //   cpu      the oracle's C restatement (oracle/liboracle.so, full pyramid) on the same epoch,
-//            one thread -- the per-thread rate of the CPU baseline;
+//            one thread -- the per-thread rate of the CPU baseline; beside it the optimised CPU
+//            form (oracle_extract_features_fast: minimal cascade, channels in AVX2 lanes);
 //   sync     the floor of one launch round trip on this box: an empty kernel + hipStreamSynchronize,
 //            and the same with a spin on hipEventQuery.
 // Prints one JSON object.
@@ -196,8 +197,25 @@ int main(int argc, char** argv) {
       cpu_med = stats(lat).med;
     }
   }
-  printf(" \"cpu_port_single_thread\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f}}\n",
+  double opt_med = 0;
+  if (h) {
+    typedef int (*fef_t)(const double*, int64_t, int32_t, int32_t, int32_t, int32_t, double*);
+    fef_t fef = (fef_t)dlsym(h, "oracle_extract_features_fast");
+    if (fef) {
+      for (int i = 0; i < 50; ++i) fef(g_epochs.data(), 1, 3, 175, 512, 16, out);
+      lat.clear();
+      for (int i = 0; i < reps; ++i) {
+        const double t0 = now_s();
+        fef(g_epochs.data() + (size_t)(i % k) * 2250, 1, 3, 175, 512, 16, out);
+        lat.push_back(now_s() - t0);
+      }
+      opt_med = stats(lat).med;
+    }
+  }
+  printf(" \"cpu_port_single_thread\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f},\n",
          cpu_med * 1e6, cpu_med > 0 ? 1.0 / cpu_med : 0.0);
+  printf(" \"cpu_optimised_single_thread\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f}}\n",
+         opt_med * 1e6, opt_med > 0 ? 1.0 / opt_med : 0.0);
   eegfx_ctx_destroy(ctx);
   return 0;
 }
