@@ -194,3 +194,111 @@ def test_vectorized_orientation_reads_as_multiplexed(tmp_path):
     assert fx.read_header(str(base) + ".vhdr").multiplexed is False
     back = fx.read_raw(str(base) + ".vhdr", str(base) + ".eeg")
     assert back.dtype == raw.dtype and np.array_equal(back, raw)
+
+
+def _random_vmrk(rng, path):
+    """A well-formed .vmrk with the variations real files show: comments, other sections holding
+    Mk-like lines, section-name case, padding around lines, "\\1" comma escapes, optional size /
+    channel / date fields, and \\n, \\r\\n or \\r line ends."""
+    eol = str(rng.choice(["\n", "\r\n", "\r"]))
+    pad = lambda: str(rng.choice(["", " ", "\t", "  "]))
+    word = "AbcS RT1x"
+    lines = ["Brain Vision Data Exchange Marker File, Version 1.0", "; comment = 1,2,3"]
+    lines += ["[Common Infos]", "Codepage=UTF-8", "DataFile=x.eeg", "Mk1=Not,a,5", ""]
+    lines.append(str(rng.choice(["[Marker Infos]", "[MARKER INFOS]", "[marker infos]"])))
+    want = []
+    for i in range(int(rng.integers(0, 40))):
+        if rng.random() < 0.15:
+            lines.append(pad() + "; Mk%d=Skipped,S  1,10" % (i + 1))
+            continue
+        typ = "".join(rng.choice(list(word), size=int(rng.integers(1, 12))))
+        desc = "".join(rng.choice(list(word + "0123456789 "), size=int(rng.integers(0, 20))))
+        if rng.random() < 0.2:
+            desc = desc[:3] + "\\1" + desc[3:]  # an escaped comma inside the description
+        p = int(rng.integers(0, 10**9))
+        fields = [typ, desc, str(p)]
+        if rng.random() < 0.8:
+            fields += [str(int(rng.integers(0, 5))), str(int(rng.integers(0, 4)))]
+            if rng.random() < 0.3:
+                fields.append("20150101120000000000")
+        lines.append(pad() + "Mk%d=%s" % (i + 1, ",".join(fields)) + pad())
+        want.append((typ, desc.replace("\\1", ","), p))
+    lines += ["", "[Other]", "Mk99=Stimulus,S  9,77"]
+    with open(path, "w", newline="") as f:
+        f.write(eol.join(lines) + eol)
+    return want
+
+
+def test_read_markers_random_files(tmp_path):
+    # The native reader against the oracle's restatement of eegloader readMarkerList on generated
+    # files (the reference holds only the two DoD recordings).
+    rng = np.random.default_rng(20)
+    for trial in range(150):
+        path = str(tmp_path / f"m{trial}.vmrk")
+        want = _random_vmrk(rng, path)
+        got = fx.read_markers(path)
+        assert oracle.read_vmrk(path) == want, trial
+        assert [(m.type, m.stimulus, m.position) for m in got] == want, trial
+        for m, (_, d, _) in zip(got, want):
+            try:
+                assert m.stimulus_index == oracle.stimulus_index(d), trial
+            except oracle.JavaError:  # Integer.parseInt overflow: flagged for the planner
+                assert m.stimulus_index == -2**31, trial
+
+
+def test_long_description_keeps_stimulus_index(tmp_path):
+    # EEGMarker descriptions are unbounded in Java; the C struct keeps 63 bytes of the text, but
+    # the stimulus index is taken from the whole description.
+    desc = "S" + " " * 70 + "12"
+    path = tmp_path / "long.vmrk"
+    path.write_text("[Marker Infos]\nMk1=Stimulus,%s,500,1,0\n" % desc)
+    (m,) = fx.read_markers(str(path))
+    assert m.stimulus_index == oracle.stimulus_index(desc) == 11
+    assert m.position == 500 and len(m.stimulus) == 63
+
+
+def test_read_header_random_files(tmp_path):
+    # The native .vhdr reader against the oracle's restatement of eegloader getChannelInfo on
+    # generated headers: key padding, section-name case, comments, "\1" escapes in channel names,
+    # missing or empty resolutions (1.0), both binary formats and orientations, and a [Comment]
+    # section whose free text must not be parsed.
+    rng = np.random.default_rng(21)
+    for trial in range(150):
+        eol = str(rng.choice(["\n", "\r\n", "\r"]))
+        n = int(rng.integers(1, 12))
+        fmt = str(rng.choice(["INT_16", "IEEE_FLOAT_32"]))
+        orient = str(rng.choice(["MULTIPLEXED", "VECTORIZED"]))
+        sp = lambda: str(rng.choice(["", " ", "\t"]))
+        lines = ["Brain Vision Data Exchange Header File Version 1.0", "; Data created by test",
+                 str(rng.choice(["[Common Infos]", "[COMMON INFOS]"])), "Codepage=UTF-8",
+                 "DataFile=x.eeg", "MarkerFile=x.vmrk", sp() + "DataOrientation=" + orient,
+                 "NumberOfChannels=%d" % n, "SamplingInterval=1000", "",
+                 "[Binary Infos]", "BinaryFormat=" + fmt, "", "[Channel Infos]",
+                 "; Ch<n>=<name>,<reference>,<resolution>,<unit>"]
+        want = []
+        for c in range(1, n + 1):
+            name = "".join(rng.choice(list("FzCPxy12"), size=int(rng.integers(1, 6))))
+            if rng.random() < 0.2:
+                name += "\\1a"
+            kind = rng.random()
+            if kind < 0.15:
+                res_txt, res = "", 1.0
+            elif kind < 0.25:
+                res_txt, res = None, 1.0
+            else:
+                res = float(rng.choice([0.1, 0.5, 1.0, 0.048828125, 10.0]))
+                res_txt = repr(res)
+            fields = [name, ""] + ([] if res_txt is None else [res_txt, "µV"])
+            lines.append(sp() + "Ch%d=%s" % (c, ",".join(fields)) + sp())
+            want.append((c, name.replace("\\1", ","), res))
+        lines += ["", "[Comment]", "Ch99=Not,a,channel", "NumberOfChannels=99"]
+        path = tmp_path / f"h{trial}.vhdr"
+        with open(path, "w", newline="", encoding="utf-8") as f:
+            f.write(eol.join(lines) + eol)
+        o = oracle.read_vhdr(str(path))
+        assert o["channels"] == want and o["n_channels"] == n, trial
+        h = fx.read_header(str(path))
+        assert h.n_channels == n, trial
+        assert h.binary_format == (0 if fmt == "INT_16" else 1), trial
+        assert h.multiplexed == (orient == "MULTIPLEXED"), trial
+        assert [(ch.number, ch.name, ch.resolution) for ch in h.channels] == want, trial
