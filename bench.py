@@ -68,6 +68,9 @@ def parse():
                          "(MLlib LogisticRegressionWithSGD, 100 full-batch iterations) on the 1M "
                          "48-dim feature rows of c3; svm: the same with SVMWithSGD")
     ap.add_argument("--chunk-frames", type=int, default=1 << 23, help="stream workload chunk")
+    ap.add_argument("--spacing", type=int, default=FRAMES_PER_EPOCH,
+                    help="c3/c32: frames between markers (default 1000, the headline; < 687 makes "
+                         "windows overlap and the window DMA cached instead of streaming)")
     ap.add_argument("--numerics", choices=["exact", "fma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
@@ -181,7 +184,10 @@ def main():
     if args.workload == "c32" and args.epochs == 1_000_000:
         args.epochs = 250_000  # 16 GB recording + 1 GB of 512-dim features per GPU
     n = args.epochs
-    n_frames = FRAMES_PER_EPOCH * n + 2000
+    sp = args.spacing
+    if sp < 100:
+        raise SystemExit("--spacing must be >= 100 frames")
+    n_frames = sp * n + 2000
     ctx = fx.Context(dev.index, numerics=args.numerics)
     # A dedicated (non-null) torch stream shared with the context: the kernels run on it, so the
     # HIP events recorded on it bracket exactly the launches of the timed region.
@@ -191,8 +197,7 @@ def main():
 
     raw = torch.empty((n_frames, ct), dtype=torch.int16, device=dev)
     ctx.synth_recording(raw, ct, SEED + rank)
-    pos = torch.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (n + 1), FRAMES_PER_EPOCH,
-                       dtype=torch.int64, device=dev)
+    pos = torch.arange(sp, sp * (n + 1), sp, dtype=torch.int64, device=dev)
     out = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
     cols, res = list(range(C)), [0.1] * C
 
@@ -262,10 +267,12 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args, raw, out, ct, C)
+        cpu = cpu_baseline(args, raw, out, ct, C, sp)
 
     if rank == 0:
         workload_key = f"fused_dwt8_c{C}_int16_{n}_{args.numerics}"
+        if sp != FRAMES_PER_EPOCH:
+            workload_key += f"_spacing{sp}"
         value = world * n * args.steps / elapsed
         achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9
         bpe = bytes_per_epoch(ct, C)
@@ -290,6 +297,7 @@ def main():
             "config": {
                 "workload": wl["desc"],
                 "epochs_per_gpu": n,
+                "marker_spacing_frames": sp,
                 "channels": C,
                 "numerics": args.numerics,
                 "kernels": kernels,
@@ -673,7 +681,7 @@ def bench_logreg(args, rank, world, dev, dist):
     ctx.close()
 
 
-def cpu_baseline(args, raw, gpu_out, ct, C):
+def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
     """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
     threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload.
 
@@ -685,8 +693,8 @@ def cpu_baseline(args, raw, gpu_out, ct, C):
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10, args.epochs)
     k1 = max(1, min(k // 25, 20000 if C == 3 else 2000))  # one-thread sample
-    host = raw[: FRAMES_PER_EPOCH * k + 2000].cpu().numpy()
-    pos = np.arange(FRAMES_PER_EPOCH, FRAMES_PER_EPOCH * (k + 1), FRAMES_PER_EPOCH, dtype=np.int64)
+    host = raw[: sp * k + 2000].cpu().numpy()
+    pos = np.arange(sp, sp * (k + 1), sp, dtype=np.int64)
     cols = list(range(C))
 
     def run(h, p, faithful, nthreads):
@@ -696,8 +704,8 @@ def cpu_baseline(args, raw, gpu_out, ct, C):
         return oracle.process_recording_fast(h, cols, [0.1] * C, p, nthreads=nthreads)
 
     def leg(n, faithful, nthreads, reps=5):
-        h = host[: FRAMES_PER_EPOCH * n + 2000]
-        run(h[: FRAMES_PER_EPOCH * 200 + 2000], pos[: min(200, n)], faithful, nthreads)
+        h = host[: sp * n + 2000]
+        run(h[: sp * 200 + 2000], pos[: min(200, n)], faithful, nthreads)
         times, feats = [], None
         for _ in range(reps):
             t0 = time.perf_counter()
