@@ -5,6 +5,9 @@
 //   hipcc ... -DFUSED_SRC='"variants/v1/fused.hip"' window_probe.hip -o window_probe_v1
 //   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
 //
+// Phase timestamps (per-workgroup s_memrealtime at each phase boundary):
+//   hipcc ... -DFUSED_SRC='"rejected/phase_timestamps/fused.hip"' -DPROBE_TIMESTAMPS ...
+//
 // Inputs are the bench workload: synth_kernel recording (configs[1]: 1M epochs x 3 ch, or
 // configs[3]: 250k epochs x 32 ch), one marker every 1,000 frames.  Prints the average launch time
 // over PROBE_ITERS launches after 200 warm-up launches (the clock settles under the power cap),
@@ -12,6 +15,7 @@
 // between variants.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -67,6 +71,49 @@ int main() {
   (void)hipEventSynchronize(b);
   float ms;
   (void)hipEventElapsedTime(&ms, a, b);
+#ifdef PROBE_TIMESTAMPS
+  {  // one more launch with per-workgroup phase timestamps (variants/ts)
+    const size_t nwg = (size_t)((n + 7) / 8);
+    unsigned long long* d_ts;
+    (void)hipMalloc(&d_ts, nwg * 5 * 8);
+    (void)hipMemset(d_ts, 0, nwg * 5 * 8);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(eegfx::dev::g_probe_ts), &d_ts, sizeof(d_ts));
+    for (int r = 0; r < 50; ++r) window();  // keep the clock at its loaded state
+    window();
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> ts(nwg * 5);
+    (void)hipMemcpy(ts.data(), d_ts, ts.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long t_min = ~0ull, t_max = 0;
+    double ph[4] = {0, 0, 0, 0};
+    size_t cnt = 0;
+    for (size_t i = 0; i < nwg; ++i) {
+      const unsigned long long* t = &ts[5 * i];
+      if (!t[0]) continue;
+      ++cnt;
+      t_min = t[0] < t_min ? t[0] : t_min;
+      t_max = t[4] > t_max ? t[4] : t_max;
+      for (int k = 0; k < 4; ++k) ph[k] += (double)(t[k + 1] - t[k]);
+    }
+    const double tick_us = 0.01;  // s_memrealtime: 100 MHz
+    printf("ts: %zu workgroups, launch span %.1f us; mean per workgroup (us): windows landed %.2f, "
+           "level 1 %.2f, levels 2-6 %.2f, rows + normalise + store %.2f, lifetime %.2f\n", cnt,
+           (t_max - t_min) * tick_us, ph[0] / cnt * tick_us, ph[1] / cnt * tick_us,
+           ph[2] / cnt * tick_us, ph[3] / cnt * tick_us,
+           (ph[0] + ph[1] + ph[2] + ph[3]) / cnt * tick_us);
+    unsigned long long* none = nullptr;  // detach before freeing: later launches must not write
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(eegfx::dev::g_probe_ts), &none, sizeof(none));
+    (void)hipDeviceSynchronize();
+    std::vector<double> ends;  // end of each workgroup relative to the first start
+    for (size_t i = 0; i < nwg; ++i)
+      if (ts[5 * i]) ends.push_back((double)(ts[5 * i + 4] - t_min) * tick_us);
+    std::sort(ends.begin(), ends.end());
+    if (!ends.empty())
+      printf("ts: workgroup end times (us from the first start): min %.1f, median %.1f, p99 %.1f, "
+             "max %.1f\n", ends.front(), ends[ends.size() / 2], ends[ends.size() * 99 / 100],
+             ends.back());
+    (void)hipFree(d_ts);
+  }
+#endif
   window();
   std::vector<double> h(n * 16 * ct);
   (void)hipMemcpy(h.data(), out, h.size() * 8, hipMemcpyDeviceToHost);
