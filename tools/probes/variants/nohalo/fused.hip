@@ -1,0 +1,550 @@
+// fused.hip -- the benchmarked hot path: multiplexed int16 recording -> dwt-8 feature matrix.
+//
+// Replaces the reference's per-epoch chain
+//   OffLineDataProvider.java:185-233  readBinaryData x3, copyOfRange, toFloatArray,
+//                                      Baseline.correct, EpochHolder.setXZ
+//   WaveletTransform.java:107-141      copy 512, eegdsp DWT, keep 16, normalize
+// without materialising the 18 KB double[3][750] epoch: only the 612 frames that reach the
+// features (100 baseline + 512 window) are read from HBM, and only the 384 B feature row is
+// written back (4,064 algorithmic bytes per epoch).
+//
+// Two launches on one stream (DESIGN.md "Kernels"):
+//
+//  baseline_kernel  the 100 pre-stimulus frames of 64 epochs are staged in LDS with aligned
+//                   16-byte loads (all issued before the first wait); lane e of wave c folds
+//                   (epoch e, channel c) sequentially in fp32 -- Baseline.java:29-42 is
+//                   order-exact, so this is deliberately not a tree reduction -- and writes
+//                   b[n][C] (12 B per epoch).  It also validates every marker position
+//                   (OffLineDataProvider.java:220-225: pos-100 in [0, n_frames]).
+//
+//  window_kernel    workgroup = C waves (wave c = channel c), sub-tile = 8 epochs x 8 lanes per
+//                   signal (dwt8.h).  The 512-frame windows arrive by LDS-DMA
+//                   (global_load_lds_dwordx4: 16-byte aligned per-lane sources, no VGPRs) into a
+//                   per-epoch LDS layout whose strides keep every half-wave of ds_read_u16 on
+//                   distinct banks; each lane folds the window's sub-16-byte misalignment into
+//                   its read base.  Lanes decode (float)raw*res - b two samples at a time just in
+//                   time inside level 1, run the cascade, and one wave normalises the 8 x 48
+//                   features (sequential sum of squares, SignalProcessing.java:38-52) and stores
+//                   them as contiguous wave stores.
+//
+// The alternatives measured against this pair (persistent and loader/consumer variants, the
+// baselines folded into the window kernel, the collapsed operator on the FP64 matrix cores) are
+// kept under tools/probes/rejected/ with their numbers in DESIGN.md §6; none of them ships.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dwt8.h"
+#include "launch.h"
+#include "lds_dma.h"
+
+namespace eegfx { namespace dev {
+// nohalo ablation (wrong results): the cascade with every cross-lane halo replaced by the lane's
+// own values, so the filter-bank instructions stay and only the ds_bpermute traffic goes.
+template <int CNT>
+__device__ __forceinline__ void halo_local(double* v) {
+  constexpr int P = CNT < 8 ? CNT : 8;
+  double h[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    h[m] = v[m % P];
+    asm volatile("" : "+v"(h[m]));  // keep it a register copy, not a folded constant
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) v[CNT + m] = h[m];
+}
+template <bool FAST>
+__device__ __forceinline__ void levels2to6_nohalo(double (&a1)[40], double& a6, double& d6) {
+  double a2[16 + 8];
+  lowpass<16, FAST>(a1, a2);
+  halo_local<16>(a2);
+  double a3[8 + 8];
+  lowpass<8, FAST>(a2, a3);
+  halo_local<8>(a3);
+  double a4[4 + 8];
+  lowpass<4, FAST>(a3, a4);
+  halo_local<4>(a4);
+  double a5[2 + 8];
+  lowpass<2, FAST>(a4, a5);
+  halo_local<2>(a5);
+  a6 = fir10<FAST, false>(a5);
+  d6 = fir10<FAST, true>(a5);
+}
+template <bool FAST, typename Fetch>
+__device__ __forceinline__ void level1_nohalo(Fetch fetch, float r, float b, double (&a1)[40]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  double x[kIn];
+  float y0[8];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+#pragma unroll
+    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
+      if (k < kSegLen) {
+        const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
+        const dwt8_f32x2 y = v * rr - bb;
+        if (k < 8) {
+          y0[k] = y.x;
+          y0[k + 1] = y.y;
+        }
+        x[k] = (double)y.x;
+        x[k + 1] = (double)y.y;
+      } else {
+        float u0 = y0[k - kSegLen], u1 = y0[k + 1 - kSegLen];
+        asm volatile("" : "+v"(u0), "+v"(u1));
+        x[k] = (double)u0;
+        x[k + 1] = (double)u1;
+      }
+    }
+    a1[i] = fir10<FAST, false>(x + 2 * i);
+  }
+}
+}}
+
+namespace eegfx {
+namespace dev {
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4_a16 __attribute__((ext_vector_type(4), aligned(16)));
+
+constexpr int kSub = 8;    // epochs per window sub-tile (8 epochs x 8 segments = 64 lanes)
+
+constexpr int round_up_res(int v, int mod, int res) {  // smallest x >= v with x % mod == res
+  return v + (((res - v % mod) % mod) + mod) % mod;
+}
+
+// LDS geometry for a CT-channel int16 recording.  Epoch e's window occupies EPQ contiguous quads
+// from dword e*ESTR: quad i holds global quad floor16(B_e) + 384*(i/25) + 16*(i%25), i.e. segment
+// s (64 frames, 384 B for CT = 3) is 25 quads = 100 dwords = 4 (mod 32) after segment s-1, the
+// 25th quad covering the misalignment.  ESTR = 1 (mod 32), so the 32 lanes of a half-wave
+// (4 epochs x 8 segments) read 32 distinct banks up to each epoch's misalignment shift.
+template <int CT>
+struct Geometry {
+  static constexpr int FB = 2 * CT;
+  static constexpr int SEGQ = kSegLen * FB / 16 + 1;     // 25
+  static constexpr int EPQ = 8 * SEGQ;                    // 200 quads per epoch
+  static constexpr int ESTR = round_up_res(EPQ * 4, 32, 1);  // 801 dwords
+  static constexpr int BASEQ = (kPre * FB + 15) / 16 + 1;    // 39 quads (600 B + misalignment)
+  static constexpr int BSTR = round_up_res(BASEQ * 4, 32, 29);  // odd, 29 (mod 32)
+  // bytes a window DMA spans from floor16(B): 7 segments + the last segment's 25 quads
+  static constexpr int64_t SPANB = (int64_t)kSegLen * FB * 7 + 16 * (SEGQ - 1) + 16;
+};
+
+// Window word of an epoch, written by baseline_kernel for window_kernel: the byte offset of its
+// 512-frame window, B = (pos + 175) * FB (even), with bit 0 set when the DMA span from floor16(B)
+// does not lie wholly inside the recording (the guarded path).  The window kernel then needs no
+// 64-bit compares on its fast path (SALU has no 64-bit ordered compare on gfx950: every such
+// test was a VALU instruction pair per epoch).
+
+__device__ __forceinline__ void lds_store4(uint32_t* dst, const u32x4_a4& v) {
+  dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+}
+
+// One 16-byte quad at byte offset A (16-aligned; may lie outside the recording): the bytes of the
+// recording it covers, zero elsewhere (Arrays.copyOfRange's zero padding).
+__device__ __forceinline__ u32x4_a4 load16(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                           int64_t A) {
+  if (A >= 0 && A + 16 <= nbytes) return *(const u32x4_a16*)(raw + A);
+  u32x4_a4 v = {0u, 0u, 0u, 0u};
+  if (A >= 0 && A < nbytes) {  // the recording ends inside this quad (even byte count)
+    uint32_t t[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; i < 4; ++i) {
+      const int64_t a = A + 4 * i;
+      if (a + 4 <= nbytes) t[i] = *(const uint32_t*)(raw + a);
+      else if (a + 2 <= nbytes) t[i] = *(const uint16_t*)(raw + a);
+    }
+    v.x = t[0]; v.y = t[1]; v.z = t[2]; v.w = t[3];
+  }
+  return v;
+}
+
+// Issue-then-consume staging: the bulk load of an in-range quad is unconditional (an out-of-range
+// lane reads a placeholder quad and discards it), so the compiler batches every load of a thread
+// before the first wait; the rare quad that straddles the end of the recording is patched
+// afterwards by load16.  NT: non-temporal read, for pre-stimulus frames no other epoch's window
+// or baseline shares (baseline_kernel 0.136 -> 0.124 ms with markers 1,000 frames apart).
+template <bool NT = false>
+__device__ __forceinline__ u32x4_a4 load16_bulk(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                                int64_t A, bool want) {
+  const bool full = want && A >= 0 && A + 16 <= nbytes;
+  const u32x4_a16* src = (const u32x4_a16*)(full ? raw + A : safe_quad(raw, nbytes));
+  u32x4_a4 v;
+  if constexpr (NT) v = __builtin_nontemporal_load(src);
+  else v = *src;
+  const u32x4_a4 z = {0u, 0u, 0u, 0u};
+  return full ? v : z;
+}
+__device__ __forceinline__ bool straddles_end(int64_t A, int64_t nbytes, bool want) {
+  return want && A >= 0 && A < nbytes && A + 16 > nbytes;
+}
+
+// Marker positions the reference cuts (OffLineDataProvider.java:220-225): copyOfRange(ch, pos-100,
+// pos+750) throws unless 0 <= pos-100 <= len.  Device-resident positions are checked here, where
+// the kernels read them anyway; a violation raises the context's error word (vector store to
+// host-mapped memory), reported as EEGFX_ERANGE by the next eegfx_ctx_synchronize.  The kernels
+// stay memory-safe for any position: an invalid one is replaced by kPre (a valid cut) before any
+// address is formed from it, so no offset arithmetic can overflow, and every read is still
+// bounds-tested or zero-filled.
+__device__ __forceinline__ bool position_ok(int64_t p, int64_t n_frames) {
+  return p >= kPre && p - kPre <= n_frames;
+}
+__device__ __forceinline__ int64_t safe_position(int64_t p, int64_t n_frames) {
+  return position_ok(p, n_frames) ? p : kPre;
+}
+__device__ __forceinline__ void flag_position(int* err) {
+  if (err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int CT, int C, int TILE, bool STREAM = false>
+__global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
+    int64_t n, float* __restrict__ bout, int64_t* __restrict__ wout, int* __restrict__ err) {
+  using G = Geometry<CT>;
+  constexpr int NT = (TILE * C + 63) / 64 * 64;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[TILE * G::BSTR];
+  __shared__ int64_t tB[TILE];
+  const int tid = threadIdx.x;
+  const int64_t nbytes = n_frames * G::FB;
+  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
+  if (tid < TILE) {
+    const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
+    if (!position_ok(p, n_frames)) flag_position(err);
+    const int64_t sp = safe_position(p, n_frames);
+    tB[tid] = (sp - kPre) * G::FB;
+    if (tid < nt) {
+      const int64_t B = (sp + 175) * G::FB;
+      const int64_t Bq = B & ~(int64_t)15;
+      wout[t0 + tid] = B | ((Bq >= 0 && Bq + G::SPANB <= nbytes) ? 0 : 1);
+    }
+  }
+  __syncthreads();
+  constexpr int ITERS = (TILE * G::BASEQ + NT - 1) / NT;
+  u32x4_a4 v[ITERS];
+  int64_t A[ITERS];
+  bool want[ITERS];
+  const bool tiny = nbytes < 16;
+#pragma unroll
+  for (int k = 0; k < ITERS; ++k) {
+    const int i = tid + k * NT;
+    const int e = i / G::BASEQ, q = i - e * G::BASEQ;
+    want[k] = i < TILE * G::BASEQ && e < nt;
+    A[k] = want[k] ? (tB[e] & ~(int64_t)15) + 16 * q : 0;
+    v[k] = load16_bulk<STREAM>(raw, nbytes, A[k], want[k] && !tiny);
+  }
+#pragma unroll
+  for (int k = 0; k < ITERS; ++k)
+    if (straddles_end(A[k], nbytes, want[k]) || (tiny && want[k])) v[k] = load16(raw, nbytes, A[k]);
+#pragma unroll
+  for (int k = 0; k < ITERS; ++k) {
+    const int i = tid + k * NT;
+    if (i < TILE * G::BASEQ) {
+      const int e = i / G::BASEQ, q = i - e * G::BASEQ;
+      lds_store4(stage + e * G::BSTR + 4 * q, v[k]);
+    }
+  }
+  __syncthreads();
+  if (tid >= TILE * C) return;
+  const int c = tid / TILE, e = tid - c * TILE;
+  const float r = sel.res[c];
+  const int16_t* src = (const int16_t*)((const uint8_t*)(stage + e * G::BSTR) + (tB[e] & 15)) +
+                       sel.col[c];
+  float b = 0.0f;
+#pragma unroll 20
+  for (int i = 0; i < kPre; ++i) b = b + (float)src[i * CT] * r;
+  if (e < nt) bout[(t0 + e) * C + c] = b / (float)kPre;
+}
+
+
+// a3 + a6 + a7 fused into level 1 (dwt8.h level1_jit): (double)((float)raw * res - b), the
+// multiply and the subtraction each one correctly rounded fp32 operation
+// (DataProviderUtils.java:49-59, Baseline.java:39-41), two samples at a time with packed fp32
+// math, read straight from the staged window: own[k*CT] for k < 64, then the 8 halo samples
+// nxt[k*CT] of the next segment.
+// FMA numerics: the 8 halo samples come from lane s+1 as decoded fp32 values (level1_jit_halo).
+template <int CT, bool FAST>
+__device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nxt, float r, float b,
+                                           int gbase, int s, double (&a1)[40]) {
+  if constexpr (FAST)
+    level1_jit_halo<FAST>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a1);
+  else
+    level1_jit<FAST>(
+        [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r,
+        b, a1);
+}
+
+// SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
+// sub-tile, executed by one wave.  `fb` holds the rows in LDS; `norm` is an 8-double LDS scratch
+// owned by the calling wave.
+//   EXACT: lane e < ne folds Math.pow(f, 2) over row e in index order (the 8 dependent chains run
+//          side by side), then the 64 lanes divide and store (16-byte stores).
+//   FMA:   (1e-9 contract) the 8 lanes of an epoch each square-sum F/8 features, a 3-step
+//          butterfly completes the row sum, and the row is scaled by 1/sqrt (rsqrt_nr: within an
+//          ulp or two of x / s; an all-zero row still gives NaN = 0 * inf); the scaled rows go
+//          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
+//          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).
+template <int F, bool FAST>
+__device__ __forceinline__ void normalise_store(double* fb, double* norm, double* o, int ne,
+                                                int lane) {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  if constexpr (FAST) {
+    static_assert(F % 16 == 0, "8 lanes per row, pairs of features");
+    constexpr int P = F / 8;
+    const int e = lane >> 3, p = lane & 7;
+    double v[P];
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      v[i] = e < ne ? fb[e * F + p * P + i] : 0.0;
+      acc = __builtin_fma(v[i], v[i], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    const double inv = rsqrt_nr(acc);
+    if (e < ne) {
+#pragma unroll
+      for (int i = 0; i < P; i += 2)
+        *(double2*)(fb + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
+    }
+    wave_sync();
+    for (int i = 2 * lane; i < ne * F; i += 128)
+      __builtin_nontemporal_store(*(const f64x2*)(fb + i), (f64x2*)(o + i));
+    wave_sync();
+    (void)norm;
+    return;
+  }
+  if (lane < ne) {
+    double acc = 0.0;
+#pragma unroll 16
+    for (int i = 0; i < F; ++i) {
+      const double f = fb[lane * F + i];
+      acc = acc + f * f;
+    }
+    norm[lane] = sqrt(acc);
+  }
+  wave_sync();
+  for (int i = 2 * lane; i < ne * F; i += 128) {
+    const double v0 = fb[i] / norm[i / F];
+    const double v1 = fb[i + 1] / norm[(i + 1) / F];
+    *(double2*)(o + i) = make_double2(v0, v1);
+  }
+  wave_sync();
+}
+
+// DMA rows of an epoch window: each row (one global_load_lds_dwordx4, lanes < SPR * SEGQ active)
+// carries SPR whole segments, so the lane's source offset is the same for every row:
+// lane l lands in segment SPR j + l / SEGQ, quad l % SEGQ, i.e. from byte
+// 64 FB (SPR j + l / SEGQ) + 16 (l % SEGQ) = (64 FB SPR) j + 16 l - (16 SEGQ - 64 FB) (l / SEGQ)
+// of floor16(B): a scalar row base plus one per-lane constant.
+template <int CT>
+struct DmaRows {
+  using G = Geometry<CT>;
+  static constexpr int SPR = 64 / G::SEGQ;                 // segments per row (2 for CT = 3)
+  static constexpr int PER_E = (8 + SPR - 1) / SPR;        // rows per epoch window (4)
+  static constexpr int LANES = SPR * G::SEGQ;              // active lanes per row (50)
+  static constexpr int ROWB = kSegLen * G::FB * SPR;       // source bytes per row (768)
+  static constexpr int ROWDW = G::SEGQ * SPR * 4;          // LDS dwords per row (200)
+  static_assert(SPR >= 1 && 8 % SPR == 0, "whole segments per row");
+  uint32_t off;
+  bool active;
+  __device__ __forceinline__ explicit DmaRows(int lane) {
+    const int sg = lane / G::SEGQ;
+    off = (uint32_t)(16 * lane - (16 * G::SEGQ - kSegLen * G::FB) * sg);
+    active = lane < LANES;
+  }
+};
+
+// Issues the LDS-DMA of one sub-tile's windows: wave w stages epochs w, w+C, w+2C, ... (every
+// DMA row of each).  The window words of those epochs are loaded (scalar: e0 and e are
+// wave-uniform, so these are lgkmcnt loads and every vector-memory counter slot stays with the
+// DMAs) before the first DMA, so the DMAs leave back to back; an epoch whose window lies wholly
+// inside the recording (bit 0 of its word clear) takes the unguarded path.  Returns whether some
+// quad of this lane could not be DMA'd (the window reaches past either end of the recording).
+template <int CT, int C, bool NT>
+__device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                          const int64_t* __restrict__ wb, int64_t e0, int ne,
+                                          uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
+  using G = Geometry<CT>;
+  constexpr int PER_E = DmaRows<CT>::PER_E;
+  constexpr int NE = (kSub + C - 1) / C;
+  int64_t W[NE];
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {  // unconditional (clamped) loads: one scalar round trip
+    const int e = w + t * C < kSub ? w + t * C : kSub - 1;
+    W[t] = wb[e0 + (e < ne ? e : ne - 1)];
+  }
+  bool need_fix = false;
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {
+    const int e = w + t * C;
+    if (e >= kSub || e >= ne) continue;  // uniform
+    const int64_t Bq = W[t] & ~(int64_t)15;
+    const uint8_t* sb = raw + Bq;
+    uint32_t* dst = win + e * G::ESTR;
+    if (((uint32_t)W[t] & 1u) == 0) {
+      if (rows.active) {
+#pragma unroll
+        for (int j = 0; j < PER_E; ++j)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
+      }
+    } else if (rows.active) {
+#pragma unroll
+      for (int j = 0; j < PER_E; ++j) {
+        const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+        if (A >= 0 && A + 16 <= nbytes)
+          dma16_s<NT>(sb + DmaRows<CT>::ROWB * j, rows.off, dst + DmaRows<CT>::ROWDW * j);
+        else need_fix = true;
+      }
+    }
+  }
+  return need_fix;
+}
+
+// Direct (non-DMA) fill of the quads dma_issue skipped (same wave -> epoch mapping): zero or
+// partial quads at either end of the recording.
+template <int CT, int C>
+__device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                          const int64_t* __restrict__ wb, int64_t e0, int ne,
+                                          uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
+  using G = Geometry<CT>;
+  constexpr int PER_E = DmaRows<CT>::PER_E;
+  for (int e = w; e < kSub; e += C) {
+    if (e >= ne) break;
+    const int64_t Bq = wb[e0 + e] & ~(int64_t)15;
+#pragma unroll
+    for (int j = 0; j < PER_E; ++j) {
+      const int64_t A = Bq + DmaRows<CT>::ROWB * j + rows.off;
+      if (rows.active && (A < 0 || A + 16 > nbytes))
+        lds_store4(win + e * G::ESTR + DmaRows<CT>::ROWDW * j + 4 * lane, load16(raw, nbytes, A));
+    }
+  }
+}
+
+// One sub-tile (8 epochs x C channels) per workgroup of C waves.  The windows land by LDS-DMA
+// (NT: non-temporal, when neighbouring windows do not overlap); after the barrier that publishes
+// them each lane decodes its 64 + 8 samples straight from LDS inside level 1, the cascade runs
+// in registers with cross-lane halos (ds_bpermute), the a6/d6 rows overwrite the start of the
+// window buffer once every wave has read its samples (26 KB of LDS per workgroup: 6 workgroups,
+// 18 waves per CU), and one wave normalises and stores the 8 rows.
+template <int CT, int C, bool FAST, bool NT>
+__global__ __launch_bounds__(64 * C, 4) void window_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
+    const float* __restrict__ base, int64_t n, double* __restrict__ out) {
+  using G = Geometry<CT>;
+  constexpr int F = C * 16;
+  static_assert(kSub * F * 8 <= kSub * G::ESTR * 4, "feature rows alias the window buffer");
+  __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
+  __shared__ double norm[kSub];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int el = lane >> 3, s = lane & 7;
+  const int64_t nbytes = n_frames * G::FB;
+  const int col = sel.col[w];
+  const float r = sel.res[w];
+  const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * kSub;
+  const int64_t rest = n - e0;  // >= 1
+  const int ne = (rest >> 31) != 0 ? kSub : ((int)rest < kSub ? (int)rest : kSub);
+
+  const bool mine = el < ne;
+  const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
+  const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
+  const DmaRows<CT> rows(lane);
+  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  dma_drain();
+  __syncthreads();
+
+  // this lane's 64 samples + 8 halo samples of signal (epoch el, channel w), decoded in level 1
+  const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col;
+  const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
+  const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
+  double a1[40], a6, d6;
+  if constexpr (FAST) {
+    level1_nohalo<FAST>([&](int k) { return (float)own[k * CT]; }, r, b, a1);
+    halo_local<32>(a1);
+    levels2to6_nohalo<FAST>(a1, a6, d6);
+  } else {
+    level1_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a1);
+    halo<32, true>(a1, nullptr, lane & ~7, s);
+    dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
+  }
+
+  double* fb = (double*)win;
+  __syncthreads();  // every wave has read its samples: the rows may overwrite the window
+  // the row slot is recomputed here from an opaque copy of the lane id, so its address is not
+  // kept live across the filter bank (it was the one spilled VGPR)
+  int l2 = lane;
+  asm volatile("" : "+v"(l2));
+  const int slot = (l2 >> 3) * F + w * 16 + (l2 & 7);
+  fb[slot] = a6;
+  fb[slot + 8] = d6;
+  __syncthreads();
+  if (w == 0) normalise_store<F, FAST>(fb, norm, out + e0 * F, ne, lane);
+}
+
+}  // namespace dev
+
+// Non-temporal (streaming) reads when the average marker spacing n_frames / n leaves the regions
+// a kernel reads (min_spacing frames per epoch) disjoint, so no other epoch would reuse the bytes
+// through L2 (markers 1,000 frames apart: window_kernel 0.918 -> 0.910 ms; 100 frames apart, where
+// each frame sits in ~6 windows: 0.777 -> 0.802 ms -- hence the test).
+bool streaming_reads(int64_t n_frames, int64_t n, int64_t min_spacing) {
+  return n > 0 && n_frames / n >= min_spacing;
+}
+
+bool fused_supported(int fmt, int ct, int C, const double* out) {
+  return fmt == 0 && ct == 3 && C == 3 && ((uintptr_t)out & 15) == 0;
+}
+
+// Scratch of the fused path: [n][C] float baselines, then (16-byte aligned) the n int64 window
+// words of baseline_kernel.
+static size_t window_words_offset(int64_t n, int C) {
+  return (sizeof(float) * (size_t)n * (size_t)C + 15) & ~(size_t)15;
+}
+size_t fused_scratch_bytes(int64_t n, int C) {
+  return window_words_offset(n, C) + sizeof(int64_t) * (size_t)n;
+}
+
+int64_t fused_window_bytes_per_epoch(int ct, int C) {
+  // window + 12 B of baselines + position + feature row
+  return (int64_t)dev::kWin * ct * 2 + (int64_t)C * 4 + 8 + (int64_t)C * 16 * 8;
+}
+
+hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
+                                 const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                                 void* scratch, int* err) {
+  if (ct != 3 || C != 3) return hipErrorNotSupported;
+  if (n == 0) return hipSuccess;
+  // 64 epochs per workgroup; 16/32/128 measured the same or slower.  Streaming
+  // reads unless another epoch's window or baseline may share the pre-stimulus frames.
+  const dim3 g((unsigned)((n + 63) / 64));
+  int64_t* words = (int64_t*)((uint8_t*)scratch + window_words_offset(n, C));
+  if (streaming_reads(n_frames, n, dev::kPre + 687))
+    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,
+                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, words, err);
+  else
+    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,
+                       n_frames, sel, pos, n, (float*)scratch, words, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
+                               const void* scratch, double* out) {
+  if (ct != 3 || C != 3) return hipErrorNotSupported;
+  if (n == 0) return hipSuccess;
+  const float* bs = (const float*)scratch;
+  const int64_t* words = (const int64_t*)((const uint8_t*)scratch + window_words_offset(n, C));
+  (void)pos;  // read by launch_fused_baseline, which wrote the window words
+  const dim3 g((unsigned)((n + dev::kSub - 1) / dev::kSub));
+  const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
+#define EEGFX_WIN(FA, NTV)                                                                         \
+  hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192), 0, st, (const uint8_t*)raw, \
+                     n_frames, sel, words, bs, n, out)
+  if (fast) { if (nt) EEGFX_WIN(true, true); else EEGFX_WIN(true, false); }
+  else { if (nt) EEGFX_WIN(false, true); else EEGFX_WIN(false, false); }
+#undef EEGFX_WIN
+  return hipGetLastError();
+}
+
+}  // namespace eegfx
