@@ -194,37 +194,101 @@ __device__ __forceinline__ void level1_jit(Fetch fetch, float r, float b, double
   }
 }
 
-// level1_jit with only the lane's own 64 samples decoded: the 8 halo samples [64(s+1), 64(s+1)+8)
-// are the fp32 values lane s+1 of the group decoded first, fetched with ds_bpermute (one dword
-// each) and widened here -- 8 fewer decodes per lane (fma numerics: 2 % fewer VALU instructions,
-// ~1 % faster; under EXACT the longer live range of y0 cost more than it saved).
-template <bool FAST, typename Fetch>
-__device__ __forceinline__ void level1_jit_halo(Fetch fetch, float r, float b, int gbase, int s,
-                                                double (&a1)[40]) {
-  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
-  const int src = gbase + ((s + 1) & (kLanesPerSignal - 1));
-  double x[kIn];
-  float y0[8];
+// FMA numerics: partial-sum halos.  The last 4 outputs of a lane's slice (t = 0..3) reach 2 + 2t
+// taps into the next lane's slice.  That lane computes those tap terms from its own first 8 values
+// and sends the 4 partial sums; the owner continues each FMA chain from the received partial over
+// its own taps.  The multiply / FMA count is fir10's, and 4 doubles cross lanes (8 ds_bpermute)
+// instead of the 8 halo values (16).  Only the summation order of those 4 outputs differs from the
+// reference's, inside the 1e-9 contract; EXACT keeps the value halos (halo / level1_jit).
+template <typename V>
+__device__ __forceinline__ void partials_for_left(const V& v, double (&p)[4]) {
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {  // output i reads x[2i .. 2i+9]
+  for (int t = 0; t < 4; ++t) {
+    double a = v(0) * tap_h(8 - 2 * t);
+#pragma unroll
+    for (int j = 9 - 2 * t; j < kTaps; ++j) a = __builtin_fma(v(j - 8 + 2 * t), tap_h(j), a);
+    p[t] = a;
+  }
+}
+__device__ __forceinline__ void pull_partials(const double (&p)[4], double (&q)[4], int gbase,
+                                              int s) {
+  const int src = gbase + ((s + 1) & (kLanesPerSignal - 1));
+#pragma unroll
+  for (int t = 0; t < 4; ++t) q[t] = __shfl(p[t], src, 64);
+}
+// output i = CNT - 4 + t of the slice: own taps j < 8 - 2t continue the received partial q
+template <typename V>
+__device__ __forceinline__ double boundary_out(const V& v, int i, int t, double q) {
+  double a = q;
+#pragma unroll
+  for (int j = 0; j < 8 - 2 * t; ++j) a = __builtin_fma(v(2 * i + j), tap_h(j), a);
+  return a;
+}
+template <int CNT>
+__device__ __forceinline__ void lowpass_ps(const double* v, double* out, int gbase, int s) {
+  static_assert(CNT >= 4, "partial-sum halos need 8 own values");
+  double p[4], q[4];
+  auto at = [&](int k) { return v[k]; };
+  partials_for_left(at, p);
+  pull_partials(p, q, gbase, s);
+#pragma unroll
+  for (int i = 0; i < CNT - 4; ++i) out[i] = fir10<true, false>(v + 2 * i);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) out[CNT - 4 + t] = boundary_out(at, CNT - 4 + t, t, q[t]);
+}
+// Levels 2..6 under FMA numerics: partial-sum halos for levels 2-4 (8+ own values per lane), value
+// halos for levels 5 and 6, whose taps span 3 and 5 lanes.
+__device__ __forceinline__ void levels2to6_ps(const double* a1, int gbase, int s, double& a6,
+                                              double& d6) {
+  double a2[16];
+  lowpass_ps<16>(a1, a2, gbase, s);
+  double a3[8];
+  lowpass_ps<8>(a2, a3, gbase, s);
+  double a4[4 + 8];
+  lowpass_ps<4>(a3, a4, gbase, s);
+  halo<4, true>(a4, nullptr, gbase, s);
+  double a5[2 + 8];
+  lowpass<2, true>(a4, a5);
+  halo<2, true>(a5, nullptr, gbase, s);
+  a6 = fir10<true, false>(a5);
+  d6 = fir10<true, true>(a5);
+}
+// Level 1 under FMA numerics with the decode fused in (as level1_jit): the lane decodes only its
+// own 64 samples; the partials its left neighbour needs are formed as soon as the first 10 are
+// decoded and leave early.  a1[0..32) receives the lane's level-1 slice.
+template <typename Fetch>
+__device__ __forceinline__ void level1_ps(Fetch fetch, float r, float b, int gbase, int s,
+                                          double (&a1)[40]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  double x[kSegLen];
+  double p[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 28; ++i) {  // outputs whose taps x[2i .. 2i+9] are all this lane's
 #pragma unroll
     for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
-      if (k < kSegLen) {
-        const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
-        const dwt8_f32x2 y = v * rr - bb;
-        if (k < 8) {
-          y0[k] = y.x;
-          y0[k + 1] = y.y;
-        }
-        x[k] = (double)y.x;
-        x[k + 1] = (double)y.y;
-      } else {
-        x[k] = (double)__shfl(y0[k - kSegLen], src, 64);
-        x[k + 1] = (double)__shfl(y0[k + 1 - kSegLen], src, 64);
-      }
+      const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
+      const dwt8_f32x2 y = v * rr - bb;
+      x[k] = (double)y.x;
+      x[k + 1] = (double)y.y;
     }
-    a1[i] = fir10<FAST, false>(x + 2 * i);
+    if (i == 0) {
+      auto at = [&](int k) { return x[k]; };
+      partials_for_left(at, p);
+      pull_partials(p, q, gbase, s);
+    }
+    a1[i] = fir10<true, false>(x + 2 * i);
   }
+  auto at = [&](int k) { return x[k]; };
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a1[28 + t] = boundary_out(at, 28 + t, t, q[t]);
+}
+// The whole cascade under FMA numerics from a fetch of the lane's own 64 samples.
+template <typename Fetch>
+__device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b, int gbase, int s,
+                                                  double& a6, double& d6) {
+  double a1[40];
+  level1_ps(fetch, r, b, gbase, s, a1);
+  levels2to6_ps(a1, gbase, s, a6, d6);
 }
 
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps
@@ -245,6 +309,11 @@ __device__ __forceinline__ void dwt8_cascade(const double (&x)[kIn], double* xch
                                              double& a6, double& d6) {
   double a1[32 + 8];
   lowpass<32, FAST>(x, a1);
+  if constexpr (FAST) {  // x already holds the level-0 halo; levels 2..6 by partial sums
+    levels2to6_ps(a1, gbase, s, a6, d6);
+    (void)xch;
+    return;
+  }
   halo<32, SHFL>(a1, xch, gbase, s);
   double a2[16 + 8];
   lowpass<16, FAST>(a1, a2);

@@ -206,16 +206,18 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
     const float r = sel.res[c];
     const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
-    double a1[40], a6, d6;
-    if constexpr (FAST)  // the 8 lanes of a group share the signal: halo samples from lane s+1
-      level1_jit_halo<FAST>([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
-                            a1);
-    else
+    double a6, d6;
+    if constexpr (FAST) {  // the 8 lanes of a group share the signal: partial-sum halos
+      dwt8_fast_cascade([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
+                        a6, d6);
+    } else {
+      double a1[40];
       level1_jit<FAST>(
           [&](int k) { return sample_at<T>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
           r, b, a1);
-    halo<32, true>(a1, nullptr, lane & ~7, s);
-    dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
+      halo<32, true>(a1, nullptr, lane & ~7, s);
+      dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
+    }
     if (valid) {
       feat[m * F + c * 16 + s] = a6;
       feat[m * F + c * 16 + 8 + s] = d6;
@@ -319,16 +321,18 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
   const float r = sel.res[c];
   const float b = base[e * C + c];
-  double a1[40], a6, d6;
-  if constexpr (FAST)
-    level1_jit_halo<FAST>([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7,
-                          s, a1);
-  else
+  double a6, d6;
+  if constexpr (FAST) {
+    dwt8_fast_cascade([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7, s,
+                      a6, d6);
+  } else {
+    double a1[40];
     level1_jit<FAST>(
         [&](int k) { return sample_at<int16_t>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
         r, b, a1);
-  halo<32, true>(a1, nullptr, lane & ~7, s);
-  dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
+    halo<32, true>(a1, nullptr, lane & ~7, s);
+    dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
+  }
   feat[c * 16 + s] = a6;
   feat[c * 16 + 8 + s] = d6;
   __syncthreads();

@@ -1,3 +1,5 @@
+// Ablation measured in round 2: builds against dwt8.h as of commit 245e12b (before the
+// partial-sum halos); kept for the record, not built by build_probes.sh.
 // fused.hip -- the benchmarked hot path: multiplexed int16 recording -> dwt-8 feature matrix.
 //
 // Replaces the reference's per-epoch chain

@@ -198,16 +198,21 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
 // (DataProviderUtils.java:49-59, Baseline.java:39-41), two samples at a time with packed fp32
 // math, read straight from the staged window: own[k*CT] for k < 64, then the 8 halo samples
 // nxt[k*CT] of the next segment.
-// FMA numerics: the 8 halo samples come from lane s+1 as decoded fp32 values (level1_jit_halo).
+// FMA numerics: dwt8_fast_cascade (own samples only; partial-sum halos); EXACT: level1_jit reads
+// the 8 halo samples of the next segment and the cascade uses value halos.
 template <int CT, bool FAST>
-__device__ __forceinline__ void level1_lds(const int16_t* own, const int16_t* nxt, float r, float b,
-                                           int gbase, int s, double (&a1)[40]) {
-  if constexpr (FAST)
-    level1_jit_halo<FAST>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a1);
-  else
+__device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* nxt, float r,
+                                            float b, int gbase, int s, double& a6, double& d6) {
+  if constexpr (FAST) {
+    dwt8_fast_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
+  } else {
+    double a1[40];
     level1_jit<FAST>(
         [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r,
         b, a1);
+    halo<32, true>(a1, nullptr, gbase, s);
+    dwt8_levels2to6<FAST, true>(a1, nullptr, gbase, s, a6, d6);
+  }
 }
 
 // SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
