@@ -236,19 +236,53 @@ __device__ __forceinline__ void lowpass_ps(const double* v, double* out, int gba
 #pragma unroll
   for (int t = 0; t < 4; ++t) out[CNT - 4 + t] = boundary_out(at, CNT - 4 + t, t, q[t]);
 }
-// Levels 2..6 under FMA numerics: partial-sum halos for levels 2-4 (8+ own values per lane), value
-// halos for levels 5 and 6, whose taps span 3 and 5 lanes.
+// Level 5 by partial sums: a5[2s + i] = sum_j h[j] a4[4s + 2i + j] takes the lane's own a4 for
+// 2i + j < 4, lane s+1's for 4 <= 2i + j < 8 and lane s+2's beyond.  Each lane computes the terms
+// it owes lanes s-1 and s-2, and the owner continues lane s+1's partial over its own taps and adds
+// lane s+2's: 4 doubles cross lanes instead of 8, for 2 adds and 2 extra multiplies.
+__device__ __forceinline__ void level5_ps(const double* a4, double* a5, int gbase, int s) {
+  double p1[2], p2[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j1 = 4 - 2 * i;  // as lane s+1 of the consumer: taps j1 .. j1+3 on a4[0..3]
+    double a = a4[0] * tap_h(j1);
+#pragma unroll
+    for (int j = j1 + 1; j < j1 + 4; ++j) a = __builtin_fma(a4[2 * i + j - 4], tap_h(j), a);
+    p1[i] = a;
+    const int j2 = 8 - 2 * i;  // as lane s+2: taps j2 .. 9 on a4[0 ..]
+    double c = a4[0] * tap_h(j2);
+#pragma unroll
+    for (int j = j2 + 1; j < kTaps; ++j) c = __builtin_fma(a4[2 * i + j - 8], tap_h(j), c);
+    p2[i] = c;
+  }
+  const int src1 = gbase + ((s + 1) & (kLanesPerSignal - 1));
+  const int src2 = gbase + ((s + 2) & (kLanesPerSignal - 1));
+  double q1[2], q2[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    q1[i] = __shfl(p1[i], src1, 64);
+    q2[i] = __shfl(p2[i], src2, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    double a = q1[i];
+#pragma unroll
+    for (int j = 0; j < 4 - 2 * i; ++j) a = __builtin_fma(a4[2 * i + j], tap_h(j), a);
+    a5[i] = a + q2[i];
+  }
+}
+// Levels 2..6 under FMA numerics: partial-sum halos for levels 2-5, value halos for level 6,
+// whose taps span 5 lanes.
 __device__ __forceinline__ void levels2to6_ps(const double* a1, int gbase, int s, double& a6,
                                               double& d6) {
   double a2[16];
   lowpass_ps<16>(a1, a2, gbase, s);
   double a3[8];
   lowpass_ps<8>(a2, a3, gbase, s);
-  double a4[4 + 8];
+  double a4[4];
   lowpass_ps<4>(a3, a4, gbase, s);
-  halo<4, true>(a4, nullptr, gbase, s);
   double a5[2 + 8];
-  lowpass<2, true>(a4, a5);
+  level5_ps(a4, a5, gbase, s);
   halo<2, true>(a5, nullptr, gbase, s);
   a6 = fir10<true, false>(a5);
   d6 = fir10<true, true>(a5);
