@@ -36,6 +36,21 @@ __global__ __launch_bounds__(256) void pattern(const uint8_t* raw, const int64_t
   }
 }
 
+// baseline span only (what baseline_kernel reads): one thread per quad, 39 quads per epoch,
+// plus one 16-byte store per epoch (baselines + window word)
+__global__ __launch_bounds__(256) void baseline_pattern(const uint8_t* raw, const int64_t* pos,
+                                                        int64_t n, u4* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = t / 39;
+  const int q = (int)(t - e * 39);
+  if (e >= n) return;
+  const int64_t b0 = ((pos[e] - 100) * 6) & ~15;
+  const u4 v = __builtin_nontemporal_load((const u4*)(raw + b0 + 16 * q));
+  const uint32_t x = v.x ^ v.y ^ v.z ^ v.w;
+  const uint32_t r = __shfl_xor(x, 1, 64) ^ x;
+  if (q == 0) out[e] = (u4){r, 0u, 0u, 0u};
+}
+
 __global__ __launch_bounds__(256) void copy(const u4* src, u4* dst, int64_t nq) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -70,6 +85,19 @@ int main() {
   const double touched = (232.0 * 16 + 8 + 384) * n;
   printf("pattern: %.4f ms  algorithmic %.1f GB/s  touched %.1f GB/s\n", ms, alg / ms / 1e6,
          touched / ms / 1e6);
+  {
+    const dim3 gb((unsigned)((n * 39 + 255) / 256));
+    hipLaunchKernelGGL(baseline_pattern, gb, dim3(256), 0, 0, raw, pos, n, (u4*)out);
+    (void)hipEventRecord(a);
+    for (int r = 0; r < 20; ++r)
+      hipLaunchKernelGGL(baseline_pattern, gb, dim3(256), 0, 0, raw, pos, n, (u4*)out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    ms /= 20;
+    printf("baseline span only: %.4f ms  algorithmic %.1f GB/s (620 B/epoch)  touched %.1f GB/s\n",
+           ms, 620.0 * n / ms / 1e6, (39.0 * 16 + 16 + 8) * n / ms / 1e6);
+  }
   const int64_t nq = nf * 6 / 32;  // copy half the recording into the other half
   hipLaunchKernelGGL(copy, dim3(4096), dim3(256), 0, 0, (const u4*)raw, (u4*)(raw + nq * 16), nq);
   (void)hipEventRecord(a);
