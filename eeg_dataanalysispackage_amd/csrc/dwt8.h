@@ -12,17 +12,19 @@
 //     level  1   2   3   4   5   6
 //     owned 32  16   8   4   2   1(a6) + 1(d6)
 // so every lane computes exactly 64 outputs (perfect balance, no idle lanes at the deep
-// levels).  Between levels each lane publishes the head of its slice in a per-lane LDS slot and
-// reads the 8-value halo of the next level from the lanes that follow it (periodic wrap inside
-// the group = the reference's periodic extension).  Everything else stays in VGPRs; only the
-// detail coefficients that reach the output (d6) are ever computed (5,120 MAC per channel
-// instead of the reference's 10,080).
+// levels).  The taps of a lane's last outputs reach into the slices of the lanes that follow it
+// (periodic wrap inside the group = the reference's periodic extension); that cross-lane data
+// moves through ds_bpermute (or, for the kernels that keep an exchange area, a per-lane LDS
+// slot).  Everything else stays in VGPRs; only the detail coefficients that reach the output (d6)
+// are ever computed (5,120 MAC per channel instead of the reference's 10,080).
 //
 // Numerics.  EXACT: every tap is one rounded fp64 multiply followed by one rounded fp64 add in
 // the reference's j = 0..9 order (the file is compiled with -ffp-contract=off), which makes the
 // coefficients bit-identical to the Java/C restatement up to the sign of an exactly-zero sum
-// (the reference starts its accumulator at +0.0).  FMA: the same chain with
-// fused multiply-adds (within 1e-9 relative of EXACT, tested).
+// (the reference starts its accumulator at +0.0); the halos carry values.  FMA:
+// fused multiply-adds, and the halos of levels 1-5 carry partial sums instead of values (the
+// following lanes sum the taps that fall on their slices; dwt8_fast_cascade / levels2to6_ps), so
+// the boundary outputs add their taps in two or three chains; within 1e-9 of EXACT, tested.
 #pragma once
 
 #include <hip/hip_runtime.h>
