@@ -196,6 +196,33 @@ __device__ __forceinline__ void level1_jit(Fetch fetch, float r, float b, double
   }
 }
 
+// Level 1 under EXACT numerics with the decode fused in: the lane decodes only its own 64 samples
+// and takes the 8 halo samples as decoded doubles from lane s+1 (its x[0..7], identical values),
+// instead of decoding them again from the next segment (24 VALU instructions per lane).
+template <typename Fetch>
+__device__ __forceinline__ void level1_exact(Fetch fetch, float r, float b, int gbase, int s,
+                                             double (&a1)[40]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  const int src = gbase + ((s + 1) & (kLanesPerSignal - 1));
+  double x[kIn];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {  // output i reads x[2i .. 2i+9]
+#pragma unroll
+    for (int k = (i == 0 ? 0 : 2 * i + 8); k < 2 * i + 10; k += 2) {
+      if (k < kSegLen) {
+        const dwt8_f32x2 v = {fetch(k), fetch(k + 1)};
+        const dwt8_f32x2 y = v * rr - bb;
+        x[k] = (double)y.x;
+        x[k + 1] = (double)y.y;
+      } else {
+        x[k] = __shfl(x[k - kSegLen], src, 64);
+        x[k + 1] = __shfl(x[k + 1 - kSegLen], src, 64);
+      }
+    }
+    a1[i] = fir10<false, false>(x + 2 * i);
+  }
+}
+
 // FMA numerics: partial-sum halos.  The last 4 outputs of a lane's slice (t = 0..3) reach 2 + 2t
 // taps into the next lane's slice.  That lane computes those tap terms from its own first 8 values
 // and sends the 4 partial sums; the owner continues each FMA chain from the received partial over

@@ -198,8 +198,8 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
 // (DataProviderUtils.java:49-59, Baseline.java:39-41), two samples at a time with packed fp32
 // math, read straight from the staged window: own[k*CT] for k < 64, then the 8 halo samples
 // nxt[k*CT] of the next segment.
-// FMA numerics: dwt8_fast_cascade (own samples only; partial-sum halos); EXACT: level1_jit reads
-// the 8 halo samples of the next segment and the cascade uses value halos.
+// FMA numerics: dwt8_fast_cascade (own samples only; partial-sum halos); EXACT: level1_exact
+// (own samples; the 8 level-1 halo samples as decoded doubles from lane s+1) and value halos.
 template <int CT, bool FAST>
 __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* nxt, float r,
                                             float b, int gbase, int s, double& a6, double& d6) {
@@ -207,9 +207,8 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
     dwt8_fast_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
   } else {
     double a1[40];
-    level1_jit<FAST>(
-        [&](int k) { return (float)(k < kSegLen ? own[k * CT] : nxt[(k - kSegLen) * CT]); }, r,
-        b, a1);
+    (void)nxt;
+    level1_exact([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a1);
     halo<32, true>(a1, nullptr, gbase, s);
     dwt8_levels2to6<FAST, true>(a1, nullptr, gbase, s, a6, d6);
   }
@@ -370,7 +369,7 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 // window buffer once every wave has read its samples (26 KB of LDS per workgroup: 6 workgroups,
 // 18 waves per CU), and one wave normalises and stores the 8 rows.
 template <int CT, int C, bool FAST, bool NT>
-__global__ __launch_bounds__(64 * C, 4) void window_kernel(
+__global__ __launch_bounds__(64 * C, 5) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
     const float* __restrict__ base, int64_t n, double* __restrict__ out) {
   using G = Geometry<CT>;

@@ -212,9 +212,8 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
                         a6, d6);
     } else {
       double a1[40];
-      level1_jit<FAST>(
-          [&](int k) { return sample_at<T>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
-          r, b, a1);
+      (void)nxt;
+      level1_exact([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s, a1);
       halo<32, true>(a1, nullptr, lane & ~7, s);
       dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
     }
@@ -327,9 +326,8 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
                       a6, d6);
   } else {
     double a1[40];
-    level1_jit<FAST>(
-        [&](int k) { return sample_at<int16_t>(k < kSegLen ? own + k * FB : nxt + (k - kSegLen) * FB); },
-        r, b, a1);
+    (void)nxt;
+    level1_exact([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7, s, a1);
     halo<32, true>(a1, nullptr, lane & ~7, s);
     dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
   }
