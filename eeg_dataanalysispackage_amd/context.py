@@ -169,7 +169,7 @@ class Context:
         cols_a, res_a = self._sel(cols, res)
         raw = _raw(raw)
         fmt = _fmt(raw)
-        n_frames = _numel(raw) // n_channels_total
+        n_frames = _frames(raw, n_channels_total)
         pos = _contig(pos, np.int64)
         n = _numel(pos)
         C = len(cols_a)
@@ -202,7 +202,7 @@ class Context:
         cols_a, res_a = self._sel(cols, res)
         raw = _raw(raw)
         fmt = _fmt(raw)
-        n_frames = _numel(raw) // n_channels_total
+        n_frames = _frames(raw, n_channels_total)
         pos = _contig(pos, np.int64)
         n = _numel(pos)
         C = len(cols_a)
@@ -225,12 +225,16 @@ class Context:
             positions = _contig(positions, np.int64)
             stimulus_index = _contig(stimulus_index, np.int32)
             n = int(positions.numel())
+            if int(stimulus_index.numel()) != n:
+                raise ValueError("positions and stimulus_index must have the same length")
             pos_out = torch.empty(max(1, n), dtype=torch.int64, device=positions.device)
             lab_out = torch.empty(max(1, n), dtype=torch.float64, device=positions.device)
         else:
             positions = np.ascontiguousarray(positions, dtype=np.int64)
             stimulus_index = np.ascontiguousarray(stimulus_index, dtype=np.int32)
             n = positions.size
+            if stimulus_index.size != n:
+                raise ValueError("positions and stimulus_index must have the same length")
             pos_out = np.empty(max(1, n), dtype=np.int64)
             lab_out = np.empty(max(1, n), dtype=np.float64)
         bal = c_int64(balance)
@@ -250,7 +254,7 @@ class Context:
             raise ValueError("process_recording_streamed takes a host recording")
         raw = np.ascontiguousarray(raw)
         fmt = _fmt(raw)
-        n_frames = raw.size // n_channels_total
+        n_frames = _frames(raw, n_channels_total)
         pos = np.ascontiguousarray(pos, dtype=np.int64)
         n = pos.size
         C = len(cols_a)
@@ -267,7 +271,7 @@ class Context:
         if not _is_device(dst):
             raise ValueError("synth_recording writes a device tensor")
         dst = _contig(dst, np.int16)
-        n_frames = dst.numel() // n_channels
+        n_frames = _frames(dst, n_channels)
         self._call(_lib.MEM_DEVICE, dst, lib().eegfx_synth_recording, self.handle, ptr(dst),
                    n_frames, n_channels, ctypes.c_uint64(seed))
 
@@ -276,6 +280,21 @@ def device_count() -> int:
     n = c_int()
     check(lib().eegfx_device_count(ctypes.byref(n)))
     return n.value
+
+
+def _frames(raw, n_channels_total: int) -> int:
+    """Frames of a multiplexed recording of n_channels_total channels: the channel count must be
+    positive, divide the buffer, and match the second dimension of a 2-D recording."""
+    ct = int(n_channels_total)
+    if ct < 1:
+        raise ValueError(f"n_channels_total must be >= 1, got {n_channels_total}")
+    shape = tuple(raw.shape)
+    if len(shape) == 2 and shape[1] != ct:
+        raise ValueError(f"recording has {shape[1]} channels per frame, n_channels_total is {ct}")
+    total = _numel(raw)
+    if total % ct:
+        raise ValueError(f"{total} samples do not divide into frames of {ct} channels")
+    return total // ct
 
 
 def _numel(a) -> int:

@@ -3,6 +3,9 @@ import os
 import re
 import subprocess
 
+import numpy as np
+import pytest
+
 import eeg_dataanalysispackage_amd as fx
 from eeg_dataanalysispackage_amd import _lib
 from conftest import REPO
@@ -93,3 +96,21 @@ def test_no_environment_knobs_in_the_product():
     for f in os.listdir(csrc):
         if f.endswith((".hip", ".cpp", ".h")):
             assert "getenv(" not in open(os.path.join(csrc, f)).read(), f
+
+
+def test_recording_frame_checks():
+    # Context methods derive n_frames from the buffer and n_channels_total; a count that does not
+    # divide the buffer, is not positive, or disagrees with a 2-D recording is refused before any
+    # device call.
+    from eeg_dataanalysispackage_amd.context import _frames
+    raw = np.zeros((100, 3), dtype=np.int16)
+    assert _frames(raw, 3) == 100
+    assert _frames(raw.reshape(-1), 3) == 100
+    assert _frames(raw.reshape(-1), 4) == 75
+    for bad in (0, -3):
+        with pytest.raises(ValueError):
+            _frames(raw, bad)
+    with pytest.raises(ValueError):
+        _frames(raw, 4)              # 2-D with 3 channels per frame
+    with pytest.raises(ValueError):
+        _frames(raw.reshape(-1), 7)  # 300 samples are not frames of 7
