@@ -342,6 +342,19 @@ def test_streamed_pinned_source_and_wide_layout(ctx_fma):
         ctx_fma.process_recording_streamed(raw, ct, cols, [0.1] * 5, pos, chunk_frames=500)
 
 
+def test_streamed_float32_recording(ctx):
+    # IEEE_FLOAT_32 samples (4-byte frames per channel) through the streamed path: chunk byte
+    # offsets scale with the frame size; unsorted positions take the reorder path.
+    rng = np.random.default_rng(31)
+    nf, ct = 30000, 4
+    raw = (rng.standard_normal((nf, ct)) * 40).astype(np.float32)
+    pos = rng.integers(100, nf + 100, size=200)
+    pos[:2] = [100, nf + 100]
+    cols, res = [3, 0], [0.5, 1.0]
+    got = ctx.process_recording_streamed(raw, ct, cols, res, pos, chunk_frames=2500)
+    assert eq(got, oracle.process_recording(raw, cols, res, pos))
+
+
 def test_vectorized_recording_through_the_provider(ctx, tmp_path):
     """OffLineDataProvider over a DataOrientation=VECTORIZED copy of DoD2015_01 gives the
     multiplexed original's epochs and features (parity unpinned against eegloader: the reference's
