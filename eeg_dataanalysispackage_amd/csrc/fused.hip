@@ -14,8 +14,9 @@
 //                   16-byte loads (all issued before the first wait); lane e of wave c folds
 //                   (epoch e, channel c) sequentially in fp32 -- Baseline.java:29-42 is
 //                   order-exact, so this is deliberately not a tree reduction -- and writes
-//                   b[n][C] (12 B per epoch).  It also validates every marker position
-//                   (OffLineDataProvider.java:220-225: pos-100 in [0, n_frames]).
+//                   b[n][C] (12 B per epoch) and each epoch's window word (byte offset of the
+//                   window + an out-of-range bit) for window_kernel.  It also validates every
+//                   marker position (OffLineDataProvider.java:220-225: pos-100 in [0, n_frames]).
 //
 //  window_kernel    workgroup = C waves (wave c = channel c), sub-tile = 8 epochs x 8 lanes per
 //                   signal (dwt8.h).  The 512-frame windows arrive by LDS-DMA
@@ -23,13 +24,15 @@
 //                   per-epoch LDS layout whose strides keep every half-wave of ds_read_u16 on
 //                   distinct banks; each lane folds the window's sub-16-byte misalignment into
 //                   its read base.  Lanes decode (float)raw*res - b two samples at a time just in
-//                   time inside level 1, run the cascade, and one wave normalises the 8 x 48
-//                   features (sequential sum of squares, SignalProcessing.java:38-52) and stores
-//                   them as contiguous wave stores.
+//                   time inside level 1 and run the cascade (fma numerics: partial-sum halos,
+//                   dwt8_fast_cascade; EXACT: value halos in the reference's order), and one wave
+//                   normalises the 8 x 48 features (EXACT: sequential sum of squares,
+//                   SignalProcessing.java:38-52) and stores them as contiguous wave stores.
 //
-// The alternatives measured against this pair (persistent and loader/consumer variants, the
-// baselines folded into the window kernel, the collapsed operator on the FP64 matrix cores) are
-// kept under tools/probes/rejected/ with their numbers in DESIGN.md §6; none of them ships.
+// The alternatives measured against this pair (persistent, work-queue, two-sub-tile and
+// loader/consumer variants, the baselines folded into the window kernel, the collapsed operator
+// on the FP64 matrix cores) are kept under tools/probes/rejected/ with their numbers in
+// DESIGN.md §6; none of them ships.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
