@@ -263,7 +263,10 @@ def main():
 
     gather = None
     if distributed and not args.no_gather:
-        gather = bench_gather(args, ctx, out, n, C, rank, world, dev, dist)
+        try:
+            gather = bench_gather(args, ctx, out, n, C, rank, world, dev, dist)
+        except Exception as exc:  # the extraction line above must still be reported
+            gather = {"op": None, "ms": None, "error": f"{type(exc).__name__}: {exc}"[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
