@@ -34,6 +34,8 @@ def bytes_per_epoch(ct, C):
     """Whole-path algorithmic bytes: 612 frames in + 8 B marker + 16*C doubles out
     (3 ch: 4,064 B; 32 ch: 43,272 B)."""
     return 612 * ct * 2 + 8 + 16 * C * 8
+
+
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFS = 78.6                    # vendor fp64 vector spec (SURVEY.md 8d; not in the guide)
 FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01/r01b_perf_study.json)

@@ -1,0 +1,40 @@
+"""bench.py's measurement plumbing on CPU: the algorithmic byte counts of SURVEY.md 8d and the
+readers of the committed profiles that fill `roofline.traffic` and `roofline.ceiling` in the
+bench line (the GPU side is timed on the box)."""
+import json
+import os
+
+import pytest
+
+import bench
+from conftest import REPO
+
+
+def test_algorithmic_bytes_per_epoch():
+    assert bench.bytes_per_epoch(3, 3) == 4064
+    assert bench.bytes_per_epoch(32, 32) == 43272     # configs[3]
+    assert bench.FLOP_PER_SIGNAL * 3 == 30720
+
+
+def test_traffic_reader_takes_the_newest_summary():
+    key = "fused_dwt8_c3_int16_1000000_fma"
+    got = bench.traffic_from_profiles(key)
+    assert got is not None and got["workload_key"] == key
+    pdir = os.path.join(REPO, "profiles")
+    names = sorted(f for f in os.listdir(pdir) if f.endswith(".json") and "traffic" in f and
+                   json.load(open(os.path.join(pdir, f))).get("workload_key") == key)
+    assert got == json.load(open(os.path.join(pdir, names[-1])))
+    # FETCH_SIZE x2 (gfx950) + WRITE_SIZE over the algorithmic 3,476 B per epoch: a few % over
+    assert 1.0 <= got["hbm_bytes_per_launch"] / 3.476e9 < 1.1
+    assert bench.traffic_from_profiles("no such workload") is None
+
+
+def test_ceiling_reader_scales_to_the_launch():
+    k = json.load(open(os.path.join(REPO, bench.CEILING_FILE)))["kernels"]["window_kernel<int16,3> fma"]
+    c = bench.ceiling_from_profiles(3, "fma", 500_000, 0.5, 1_738_000_000)
+    assert c["ms"] == pytest.approx(k["ceiling_ms"] * 500_000 / k["epochs_per_launch"], abs=1e-4)
+    assert c["frac"] == pytest.approx(1.738e9 / (c["ms"] * 1e-3) / 8e12, rel=1e-3)
+    assert c["kernel_over_ceiling"] == pytest.approx(c["ms"] / 0.5, rel=1e-3)
+    assert 0.5 < c["frac"] < 0.8            # the measured power-capped bound, not HBM's 1.0
+    assert bench.ceiling_from_profiles(3, "exact", 1, 1.0, 1) is None
+    assert bench.ceiling_from_profiles(7, "fma", 1, 1.0, 1) is None
