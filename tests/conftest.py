@@ -23,6 +23,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libeegfx on the device)")
 
 
+# Run order under `pytest -x`: the golden / oracle parity tests first, so that a failure in a
+# heavy test (the 48 GB configs[2] shard, the multi-process rehearsals) can never leave them
+# unreached; everything else keeps its collection order inside its rank.
+_FIRST = ("test_oracle_golden", "test_library_abi", "test_gpu_parity", "test_gpu_c_abi",
+          "test_gpu_fuzz", "test_gpu_fuzz_fused")
+_LAST = ("test_gpu_distributed", "test_gpu_configs2")
+
+
+def _rank(item):
+    mod = os.path.splitext(os.path.basename(str(item.fspath)))[0]
+    if mod in _FIRST:
+        return _FIRST.index(mod)
+    if mod in _LAST:
+        return 100 + _LAST.index(mod)
+    return 50
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=_rank)  # stable: collection order is kept within a module and a rank
+
+
 @pytest.fixture(scope="session")
 def golden_vectors():
     with open(os.path.join(GOLDEN, "golden_vectors.json")) as f:
