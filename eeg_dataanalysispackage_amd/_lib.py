@@ -156,9 +156,15 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+class EegfxRangeError(EegfxError, IndexError):
+    """ERANGE: a marker position the reference would not cut (OffLineDataProvider.java:220-225,
+    copyOfRange's ArrayIndexOutOfBoundsException) -- an IndexError that keeps the status code."""
+
+
 def check(rc: int) -> None:
     if rc != EEGFX_OK:
-        raise EegfxError(rc, lib().eegfx_last_error().decode(errors="replace"))
+        msg = lib().eegfx_last_error().decode(errors="replace")
+        raise (EegfxRangeError if rc == EEGFX_ERANGE else EegfxError)(rc, msg)
 
 
 def ptr(a) -> c_void_p:

@@ -19,7 +19,7 @@ from typing import Dict, Optional, Sequence
 
 import numpy as np
 
-from ._lib import EegfxError, check, lib, ptr
+from ._lib import EegfxError, lib, ptr
 from .context import Context, _contig, _is_device, _mem
 
 # LogisticRegressionWithSGD() defaults (MLlib 1.6.2) and GradientDescent's convergence tolerance
@@ -42,9 +42,11 @@ def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini
     w = (np.zeros(d) if initial_weights is None
          else np.array(initial_weights, dtype=np.float64).copy())
     it = c_int32()
-    check(getattr(lib(), entry)(ctx.handle, ptr(X), ptr(y), n, d, int(num_iterations),
-                                float(step_size), float(reg_param), float(mini_batch_fraction),
-                                float(convergence_tol), ptr(w), byref(it), _mem(X, y)))
+    mem = _mem(X, y)
+    # ordered after the torch work that produced X / y (Context._call), like every device call
+    ctx._call(mem, X, getattr(lib(), entry), ctx.handle, ptr(X), ptr(y), n, d,
+              int(num_iterations), float(step_size), float(reg_param),
+              float(mini_batch_fraction), float(convergence_tol), ptr(w), byref(it), mem)
     return w, it.value
 
 
@@ -58,8 +60,9 @@ def _predict(entry, ctx: Context, X, weights, intercept, threshold):
     else:
         out = np.empty(n, dtype=np.float64)
     t = math.nan if threshold is None else float(threshold)
-    check(getattr(lib(), entry)(ctx.handle, ptr(X), n, d, ptr(w), float(intercept), t, ptr(out),
-                                _mem(X, out)))
+    mem = _mem(X, out)
+    ctx._call(mem, X, getattr(lib(), entry), ctx.handle, ptr(X), n, d, ptr(w), float(intercept),
+              t, ptr(out), mem)
     return out
 
 

@@ -7,7 +7,8 @@ ordered with torch's current stream on both sides: the context stream waits for 
 produced the inputs, and torch's stream waits for the kernels before anything later uses (or
 frees) the buffers.  Marker positions held in device memory are validated by the kernels; a
 violation raises ``IndexError`` (the reference's ArrayIndexOutOfBoundsException) from the next
-``Context.synchronize()``.
+call that synchronises the context (``Context.synchronize()``, or any host-memory call); device
+results are unspecified until such a call has returned without error.
 """
 from __future__ import annotations
 
@@ -130,10 +131,7 @@ class Context:
     def synchronize(self) -> None:
         """Waits for the context stream.  Raises IndexError when a kernel met a device-resident
         marker position the reference would not cut (OffLineDataProvider.java:220-225)."""
-        rc = lib().eegfx_ctx_synchronize(self.handle)
-        if rc == _lib.EEGFX_ERANGE:
-            raise IndexError(lib().eegfx_last_error().decode(errors="replace"))
-        check(rc)
+        check(lib().eegfx_ctx_synchronize(self.handle))  # ERANGE -> EegfxRangeError (IndexError)
 
     def kernel_stats(self):
         """(timed launches, summed duration in ms, algorithmic bytes) of the dominant kernel

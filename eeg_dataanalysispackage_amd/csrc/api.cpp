@@ -203,6 +203,21 @@ struct eegfx_ctx {
   }
 
   void activate() const { HIP_CHECK(hipSetDevice(device)); }
+  // Waits for the stream, then reports (and clears) a device-resident marker position that a
+  // kernel enqueued on this context since the last check refused: every API call that
+  // synchronises does this, so an invalid position surfaces at the first synchronising call
+  // after it (at the latest eegfx_ctx_synchronize), never silently.
+  void check_positions_flag() {
+    if (__atomic_exchange_n(err_host, 0, __ATOMIC_ACQ_REL) != 0)
+      fail(EEGFX_ERANGE,
+           "a device-resident marker position lies outside [100, n_frames + 100] "
+           "(OffLineDataProvider.java:220-225: ArrayIndexOutOfBoundsException); the rows of such "
+           "epochs are unspecified");
+  }
+  void drain() {
+    HIP_CHECK(hipStreamSynchronize(stream));
+    check_positions_flag();
+  }
   void tic() {
     if (!timing) return;
     if (n_timed == events.size()) {
@@ -474,7 +489,7 @@ struct eegfx_odp {
     HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, h.info.binary_format, n_frames, ct, sel, 3,
                                 d_pos, k, (double*)((char*)d_epochs + per * (size_t)n_epochs),
                                 ctx->fused.get(fused_scratch_bytes(k, 3)), ctx->err_dev));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->drain();
     n_epochs += k;
     positions.insert(positions.end(), pos.begin(), pos.end());
     labels.insert(labels.end(), lab.begin(), lab.end());
@@ -601,12 +616,7 @@ int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
   return guarded([&] {
     if (!ctx) fail(EEGFX_EINVAL, "null context");
     ctx->activate();
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (__atomic_exchange_n(ctx->err_host, 0, __ATOMIC_ACQ_REL) != 0)
-      fail(EEGFX_ERANGE,
-           "a device-resident marker position lies outside [100, n_frames + 100] "
-           "(OffLineDataProvider.java:220-225: ArrayIndexOutOfBoundsException); the rows of such "
-           "epochs are unspecified");
+    ctx->drain();
   });
 }
 
@@ -663,7 +673,7 @@ int eegfx_read_raw(eegfx_ctx* ctx, const char* vhdr_path, const char* eeg_path, 
       std::vector<char> host((size_t)bytes);
       read_recording(h, eeg_path, host.data(), n);
       HIP_CHECK(hipMemcpyAsync(dst, host.data(), (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      ctx->drain();
     }
   });
 }
@@ -692,7 +702,7 @@ int eegfx_cut_epochs_f64(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n
     ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(epochs_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      ctx->drain();
     }
   });
 }
@@ -734,6 +744,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
                                         (double*)ctx->pin_out.device_ptr()));
         ctx->toc(0);
         ctx->wait_small();
+        ctx->check_positions_flag();
         memcpy(out, hout, out_bytes);
         return;
       }
@@ -758,7 +769,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
       }
       ctx->toc(0);
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      ctx->drain();
       return;
     }
     const double* d_in = (const double*)stage_in(ctx, ctx->scratch, epochs, in_bytes, mem);
@@ -769,7 +780,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
     ctx->toc(0);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      ctx->drain();
     }
   });
 }
@@ -795,7 +806,7 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
     run_features_from_raw(ctx, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(features, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      ctx->drain();
     }
   });
 }
@@ -881,7 +892,7 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
     try {
       for (int b = 0; b < 2; ++b)
         if (!pinned) HIP_CHECK(hipHostMalloc(&pin[b], cbytes, hipHostMallocDefault));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));  // d_pos uploaded; buffers idle
+      ctx->drain();  // d_pos uploaded; buffers idle
       int64_t i = 0, k = 0;
       while (i < n) {
         const int b = (int)(k % R);
@@ -923,12 +934,13 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
         std::vector<double> sorted((size_t)(n * F));
         HIP_CHECK(hipMemcpyAsync(sorted.data(), d_out, sizeof(double) * sorted.size(),
                                  hipMemcpyDeviceToHost, ctx->stream));
-        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->drain();
         for (int64_t r = 0; r < n; ++r)
           memcpy(features + order[(size_t)r] * F, sorted.data() + r * F,
                  sizeof(double) * (size_t)F);
       }
       HIP_CHECK(hipStreamSynchronize(cs));
+      ctx->drain();
     } catch (...) {
       (void)hipStreamSynchronize(ctx->stream);
       if (cs) (void)hipStreamSynchronize(cs);
@@ -985,7 +997,7 @@ static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double
       HIP_CHECK(launch_lr_iteration(ctx->stream, grad, dX, dy, n, d, st, part, G, step_size,
                                     reg_param, convergence_tol, num_iterations));
     HIP_CHECK(hipMemcpyAsync(hs.data(), st, sbytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->drain();
     if (h->converged == 2) fail(EEGFX_EINVAL, "Input validation failed: labels must be 0.0 or 1.0");
     memcpy(weights, h->w, sizeof(double) * (size_t)d);
     if (iterations_run) *iterations_run = h->iter;
@@ -1021,7 +1033,7 @@ static int glm_predict(int grad, eegfx_ctx* ctx, const double* X, int64_t n, int
     if (mem == EEGFX_MEM_HOST)
       HIP_CHECK(hipMemcpyAsync(out, dout, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost,
                                ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->drain();
   });
 }
 
@@ -1092,7 +1104,7 @@ int eegfx_plan_markers_device(eegfx_ctx* ctx, const int64_t* positions,
         HIP_CHECK(hipMemcpyAsync(label_out, d_label, sizeof(double) * (size_t)r.selected,
                                  hipMemcpyDeviceToHost, ctx->stream));
     }
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->drain();
     *balance = r.balance;
     *n_selected = r.selected;
     if (r.first_unparsable >= 0)  // Integer.parseInt's NumberFormatException ends the reference loop
@@ -1150,7 +1162,7 @@ int eegfx_odp_get_data(const eegfx_odp* odp, double* out) {
     HIP_CHECK(hipMemcpyAsync(out, odp->d_epochs,
                              sizeof(double) * 3 * EEGFX_POSTSTIMULUS * (size_t)odp->n_epochs,
                              hipMemcpyDeviceToHost, odp->ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(odp->ctx->stream));
+    odp->ctx->drain();
   });
 }
 
@@ -1184,7 +1196,7 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
                                           odp->n_epochs, 3, skip, feature_size,
                                           ctx->numerics != EEGFX_EXACT, d_out));
     HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->drain();
   });
 }
 

@@ -139,6 +139,11 @@ __global__ __launch_bounds__(256) void features_from_epochs_kernel(const double*
 // stages them in LDS, runs the filter bank (wave = 8 channels x 8 segments), normalises, and
 // writes the row back across the link.  C <= kSmallMaxC.
 constexpr int kSmallMaxC = 16;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "features_small_kernel stages 66 KB of LDS per workgroup: gfx950 (160 KB per CU) only"
+#endif
+static_assert(sizeof(double) * (kSmallMaxC * kWin + kSmallMaxC * 16 + 1) <= 160 * 1024,
+              "features_small_kernel's LDS exceeds one gfx950 CU");
 template <bool FAST>
 __global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
                                                              int64_t n, int C, int nfeat,

@@ -23,8 +23,11 @@
  * device pointers, the work is enqueued on the context stream and the call returns without
  * synchronising -- call eegfx_ctx_synchronize()).  Device-resident marker positions are
  * validated by the kernels that read them (OffLineDataProvider.java:220-225: pos-100 must lie
- * in [0, n_frames]); a violation is reported as EEGFX_ERANGE by the next eegfx_ctx_synchronize
- * (host positions are checked before any work is enqueued and fail the call itself).
+ * in [0, n_frames]); a violation is reported as EEGFX_ERANGE by the next call on that context
+ * that synchronises it -- eegfx_ctx_synchronize, or any EEGFX_MEM_HOST compute call -- which
+ * also clears it.  Results of EEGFX_MEM_DEVICE calls are unspecified until such a call has
+ * returned EEGFX_OK.  Host positions are checked before any work is enqueued and fail the call
+ * itself.
  */
 #ifndef EEGFX_H_
 #define EEGFX_H_
@@ -78,7 +81,9 @@ int eegfx_device_count(int* count);
 int eegfx_ctx_create(int device, eegfx_ctx** out);
 /* Makes the context enqueue on `hip_stream` (hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream.  The previous stream is drained first (the context's
- * device buffers are allocated and released in its stream's order). */
+ * device buffers are allocated and released in its stream's order).  The context keeps using an
+ * external stream until told otherwise -- eegfx_ctx_destroy drains and frees on it too -- so call
+ * eegfx_ctx_set_stream(ctx, NULL) before the caller destroys that stream. */
 int eegfx_ctx_set_stream(eegfx_ctx* ctx, void* hip_stream);
 /* The stream the context currently enqueues on (hipStream_t). */
 int eegfx_ctx_stream(eegfx_ctx* ctx, void** hip_stream);

@@ -75,6 +75,33 @@ def test_predict(ctx):
     assert np.array_equal(pd.cpu().numpy(), p)
 
 
+def test_device_inputs_order_with_torch_stream():
+    """X / y produced by torch kernels still queued behind busy matmuls, passed straight to
+    sgd_train / predict on a fresh context (its own non-blocking stream): no synchronisation by
+    the caller anywhere."""
+    c = fx.Context(0, numerics="exact")
+    X, y = rows(20000, 48, 23)
+    wr, itr = ref.sgd_train(X, y, 100, 1.0, 0.0)
+    score = ref.predict(X, wr, threshold=None)
+    Xd0, yd0 = torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda()
+    torch.cuda.synchronize()
+    for it in range(3):
+        big = torch.randn((4096, 4096), device="cuda")
+        for _ in range(3):
+            big = big @ big
+            big = big / big.abs().max()
+        zero = big[:1, :1].double() * 0.0
+        Xd = Xd0 * 1.0 + zero          # both queued behind the matmuls
+        yd = yd0 + zero[0]
+        w, n_it = clf.sgd_train(c, Xd, yd, 100, 1.0, 0.0)
+        assert n_it == itr and close(w, wr), it
+        Xp = Xd0 * 1.0 + zero
+        s = clf.predict(c, Xp, wr, threshold=None)
+        got = (s * 1.0).cpu().numpy()  # consumed by torch right away
+        assert np.max(np.abs(got - score)) <= 1e-12, it
+    c.close()
+
+
 def test_errors(ctx):
     X, y = rows(50, 48, 3)
     y[7] = 2.0

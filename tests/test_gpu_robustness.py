@@ -72,6 +72,26 @@ def test_invalid_device_positions_raise_at_synchronize(ctx, ct, cols):
         assert eq(out.cpu().numpy(), oracle.process_recording(raw, cols, [0.1] * len(cols), [edge]))
 
 
+def test_invalid_device_position_surfaces_at_next_synchronising_call(ctx):
+    """A caller that never calls synchronize() still sees the refused position: the next API call
+    that synchronises the context (here a host-memory call) raises IndexError (ERANGE), clears
+    the flag, and the call after it is exact again."""
+    rng = np.random.default_rng(8)
+    nf = 30_000
+    raw = synth_raw(rng, nf, 3)
+    good = rng.integers(100, nf - 900, size=20).astype(np.int64)
+    bad = good.copy()
+    bad[3] = 42
+    ctx.process_recording(torch.from_numpy(raw).to(DEV), 3, [0, 1, 2], [0.1] * 3,
+                          torch.from_numpy(bad).to(DEV))
+    with pytest.raises(IndexError) as e:
+        ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, good)
+    assert e.value.code == -6
+    got = ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, good)
+    assert eq(got, oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, good))
+    ctx.synchronize()
+
+
 def test_invalid_device_positions_in_cut_epochs(ctx):
     rng = np.random.default_rng(5)
     raw = synth_raw(rng, 20_000, 3)
@@ -186,3 +206,27 @@ def test_small_batches_zero_copy_path(ctx):
         assert eq(ctx.extract_features(ep[i:i + 1]), want[i:i + 1]), i
     fe = fx.WaveletTransform(context=ctx)
     assert eq(fe.extractFeatures(ep[0]), want[0])
+
+
+@pytest.mark.parametrize("C", [3, 5, 9, 16])
+def test_small_batches_every_channel_count_both_numerics(C):
+    """The zero-copy small-batch kernel (features_small_kernel) for channel counts that use one
+    wave (C <= 8) and two waves (C = 9..16), under EXACT (value-exact) and FMA numerics (its
+    dwt8_cascade<true, true> partial-sum halos; <= 1e-9 per normalised feature)."""
+    rng = np.random.default_rng(100 + C)
+    raw = synth_raw(rng, 60_000, C)
+    cols = list(range(C))
+    pos = rng.integers(100, 59_000, size=9).astype(np.int64)
+    ep = oracle.decode_epochs(raw, cols, [0.1] * C, pos)
+    want = oracle.extract_features(ep)
+    for numerics in ("exact", "fma"):
+        c = fx.Context(0, numerics=numerics)
+        try:
+            for n in (1, 2, 9):
+                got = c.extract_features(ep[:n])
+                if numerics == "exact":
+                    assert eq(got, want[:n]), (C, n)
+                else:
+                    assert np.max(np.abs(got - want[:n])) <= 1e-9, (C, n)
+        finally:
+            c.close()
