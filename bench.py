@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark of the epoch-to-feature hot path (BASELINE.json metric, configs[1] per GPU).
 
-One step = one launch of the fused raw -> dwt-8 feature kernel over one batch of 1,000,000
-synthetic epochs (3 channels, multiplexed int16 @ 1000 Hz, one marker every 1000 frames),
-inputs already resident in HBM.  N GPUs = N ranks (torch.distributed, RCCL), each with its own
-recording of the same shape (weak scaling: epochs are independent, no data-path collective).
+One step = one pass of the fused raw -> dwt-8 feature kernels over one batch of synthetic epochs
+(3 channels, multiplexed int16 @ 1000 Hz, one marker every 1000 frames), inputs already resident
+in HBM: 1,000,000 epochs at N = 1 (configs[1]); at N > 1 every rank (torch.distributed, RCCL)
+extracts its own 8,000,000-epoch shard, so N = 8 is configs[2]'s 64M epochs (weak scaling:
+epochs are independent, no data-path collective).  The feature gather to rank 0 is timed after
+the extraction steps and reported beside `value` (`gather`, `extract_plus_gather`).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--numerics exact|fma]
 
@@ -46,6 +48,10 @@ WINDOW_KERNEL = "window_kernel<int16,3>"
 WORKLOADS = {
     "c3": {"ct": 3, "C": 3, "desc": "configs[1]: synthetic 1M epochs x 3 ch (Fz/Cz/Pz) multiplexed "
                                     "int16 @1000 Hz -> fe=dwt-8 48-dim L2-normalised features, per GPU"},
+    "c3dist": {"ct": 3, "C": 3, "desc": "configs[2]: synthetic multiplexed int16 recordings, "
+                                        "3 ch (Fz/Cz/Pz) @1000 Hz, epoch-sharded over the GPUs, "
+                                        "8M epochs per rank (64M over 8xMI355X) -> fe=dwt-8 "
+                                        "48-dim L2-normalised features"},
     "c32": {"ct": 32, "C": 32, "desc": "configs[3]: synthetic epochs x full 32-channel montage, "
                                        "multiplexed int16 @1000 Hz, every channel through the DWT -> "
                                        "512-dim L2-normalised features, per GPU"},
@@ -58,7 +64,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps; ~50 ms of sustained load brings the clocks to their steady (power-capped) state")
-    ap.add_argument("--epochs", type=int, default=1_000_000, help="epochs per GPU per step")
+    ap.add_argument("--epochs", type=int, default=None,
+                    help="epochs per GPU per step (default: 1,000,000 = configs[1] at N = 1; "
+                         "8,000,000 per rank = configs[2]'s 64M epochs over 8 GPUs when N > 1)")
     ap.add_argument("--workload", choices=["c3", "c32", "stream", "dropin", "logreg", "svm"],
                     default="c3",
                     help="c3: configs[1] (Fz/Cz/Pz, 48-dim, the headline); c32: configs[3] (full "
@@ -182,9 +190,16 @@ def main():
     if args.workload in ("logreg", "svm"):
         return bench_logreg(args, rank, world, dev, dist if distributed else None)
     wl = WORKLOADS[args.workload]
+    if args.workload == "c3" and distributed:
+        wl = WORKLOADS["c3dist"]  # the N > 1 line is configs[2]: 8M epochs per rank
     ct, C = wl["ct"], wl["C"]
-    if args.workload == "c32" and args.epochs == 1_000_000:
-        args.epochs = 250_000  # 16 GB recording + 1 GB of 512-dim features per GPU
+    if args.epochs is None:
+        if args.workload == "c32":
+            args.epochs = 250_000  # 16 GB recording + 1 GB of 512-dim features per GPU
+        elif distributed:
+            args.epochs = 8_000_000  # 48 GB recording + 3.07 GB of features per rank
+        else:
+            args.epochs = 1_000_000
     n = args.epochs
     sp = args.spacing
     if sp < 100:
@@ -341,7 +356,7 @@ def main():
         if gather:
             line["gather"] = gather
             if gather.get("ms") is not None:
-                # extract + gather: every rank ends holding the whole feature matrix
+                # extract + gather: the whole feature matrix on rank 0 (the product leg)
                 line["extract_plus_gather"] = {
                     "value": round(world * n / ((elapsed / args.steps) + gather["ms"] * 1e-3), 1),
                     "unit": "epochs/s", "gather_op": gather["op"]}
@@ -354,13 +369,16 @@ def main():
 
 def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
     """The only exchange of the path: assembling the [world*n][16C] feature matrix
-    in rank (= getData()) order on every rank.  Product leg: eegfx_gather through the C ABI (one
-    RCCL broadcast per rank inside a group, over xGMI), on a communicator created from an RCCL
-    unique id that rank 0 ships over the torch process group.  Comparison leg: torch's
-    all_gather_into_tensor (+ pad / concat for ragged shards).  Both are timed outside the
-    extraction steps (2 warm + 5 timed, max over ranks) and every rank checks its own rows."""
+    in rank (= getData()) order.  Product leg: eegfx_gather_root through the C ABI -- the matrix
+    on rank 0 only, the reference's single consumer (OffLineDataProvider.java:370-372,
+    LogisticRegressionClassifier.java:87-94) -- by grouped RCCL send/recv over xGMI, every shard
+    crossing one link once, on a communicator created from an RCCL unique id that rank 0 ships
+    over the torch process group.  Beside it: eegfx_gather (the matrix on every rank, one RCCL
+    broadcast per rank), and the same two exchanges through torch.distributed
+    (isend/irecv to rank 0; all_gather_into_tensor + pad / concat).  All are timed outside the
+    extraction steps (2 warm + 5 timed, max over ranks) and check the rows they deliver."""
     import torch
-    from eeg_dataanalysispackage_amd.sharding import Comm, gather_features
+    from eeg_dataanalysispackage_amd.sharding import Comm, gather_features, gather_features_root
 
     def timed(fn, reps=5):
         fn()
@@ -375,20 +393,40 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return res, float(t[0]) * 1e3
 
-    res = {"bytes_per_rank": n * 16 * C * 8, "rows": world * n}
+    def root_ok(full):
+        """rank 0 holds every rank's rows in rank order: its own rows bit-equal, the others unit
+        rows (each rank checks its own rows in the all-ranks legs)."""
+        if rank != 0:
+            return full is None
+        norms = torch.linalg.vector_norm(full, dim=1)
+        return bool(torch.equal(full[:n], out) and torch.max(torch.abs(norms - 1)) < 1e-12)
+
+    bpr = n * 16 * C * 8
+    res = {"bytes_per_rank": bpr, "rows": world * n, "root": 0,
+           "root_inbound_bytes": bpr * (world - 1)}
     if args.dist_backend == "nccl":
         uid = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(ctx, world, rank, uid[0])
+        full = (torch.empty((world * n, 16 * C), dtype=torch.float64, device=dev)
+                if rank == 0 else None)
+        got, ms = timed(lambda: comm.gather_root(out, world * n, root=0, out=full))
+        res.update({"op": "eegfx_gather_root (RCCL grouped send/recv to rank 0)",
+                    "ms": round(ms, 3), "rows_check": root_ok(got),
+                    "root_inbound_GBps": round(bpr * (world - 1) / (ms * 1e-3) / 1e9, 1)})
+        del full, got
         full = torch.empty((world * n, 16 * C), dtype=torch.float64, device=dev)
-        full, ms = timed(lambda: comm.gather(out, world * n, out=full))
-        ok = bool(torch.equal(full[rank * n:(rank + 1) * n], out))
+        full, ms_b = timed(lambda: comm.gather(out, world * n, out=full))
+        res["all_ranks"] = {"op": "eegfx_gather (RCCL broadcast per rank, grouped)",
+                            "ms": round(ms_b, 3),
+                            "rows_check": bool(torch.equal(full[rank * n:(rank + 1) * n], out))}
         comm.close()
         del full
-        res.update({"op": "eegfx_gather (RCCL broadcast per rank, grouped)", "ms": round(ms, 3),
-                    "rows_check": ok})
+        got, ms_r = timed(lambda: gather_features_root(out, world * n, 0))
+        res["torch_root_p2p"] = {"ms": round(ms_r, 3), "rows_check": root_ok(got)}
+        del got
     else:
-        res.update({"op": None, "ms": None, "note": "C-ABI gather needs RCCL (rehearsal backend)"})
+        res.update({"op": None, "ms": None, "note": "C-ABI gathers need RCCL (rehearsal backend)"})
     full, ms_t = timed(lambda: gather_features(out, world * n))
     res["torch_all_gather"] = {"ms": round(ms_t, 3),
                                "rows_check": bool(torch.equal(full[rank * n:(rank + 1) * n], out))}
@@ -608,7 +646,7 @@ def bench_logreg(args, rank, world, dev, dist):
     svm = args.workload == "svm"
     train = clf.svm_sgd_train if svm else clf.sgd_train
     algo = "SVMWithSGD" if svm else "LogisticRegressionWithSGD"
-    n = args.epochs
+    n = args.epochs or 1_000_000
     ctx = fx.Context(dev.index, numerics=args.numerics)
     raw = torch.empty((FRAMES_PER_EPOCH * n + 2000, 3), dtype=torch.int16, device=dev)
     ctx.synth_recording(raw, 3, SEED + rank)

@@ -56,6 +56,13 @@ class Marker(Structure):
                 ("stimulus_index", c_int32)]
 
 
+class GatherOp(Structure):
+    _fields_ = [("kind", c_int32), ("peer", c_int32), ("row", c_int64), ("rows", c_int64)]
+
+
+GATHER_SEND, GATHER_RECV, GATHER_COPY = 0, 1, 2
+
+
 class EegfxError(RuntimeError):
     """A non-zero status of the C ABI (carries the code and eegfx_last_error())."""
 
@@ -112,6 +119,9 @@ SIGNATURES = {
     "eegfx_comm_init_all": (c_int, [POINTER(c_void_p), c_int32, POINTER(c_void_p)]),
     "eegfx_comm_rank": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "eegfx_gather": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    "eegfx_gather_root": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
+    "eegfx_gather_root_plan": (c_int, [c_int64, c_int32, c_int32, c_int32, POINTER(GatherOp),
+                                       POINTER(c_int32)]),
     "eegfx_group_start": (c_int, []),
     "eegfx_group_end": (c_int, []),
     "eegfx_comm_destroy": (c_int, [c_void_p]),

@@ -8,6 +8,8 @@
 // row (eegfx_shard_range), and a rooted broadcast writes each shard straight into its final rows
 // of `out` with no padding or compaction pass.  RCCL runs over xGMI (peer-to-peer links) on an
 // MI355X node.  Normalisation is per row, so there is no statistic to all-reduce.
+// eegfx_gather_root assembles the matrix on one rank only (the reference's single consumer):
+// grouped ncclSend / ncclRecv, every shard crossing one xGMI link once.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -145,6 +147,65 @@ int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t
     }
     const ncclResult_t g = ncclGroupEnd();
     nccl_check(r, "ncclBroadcast");
+    nccl_check(g, "ncclGroupEnd");
+  });
+}
+
+int eegfx_gather_root_plan(int64_t n_total, int32_t world, int32_t rank, int32_t root,
+                           eegfx_gather_op* ops, int32_t* n_ops) {
+  return guarded([&] {
+    if (n_total < 0 || world < 1 || rank < 0 || rank >= world || root < 0 || root >= world ||
+        !ops || !n_ops)
+      fail(EEGFX_EINVAL, "gather_root_plan(n=%lld, world=%d, rank=%d, root=%d)",
+           (long long)n_total, world, rank, root);
+    int k = 0;
+    for (int r = 0; r < world; ++r) {
+      int64_t s = 0, e = 0;
+      shard(n_total, world, r, &s, &e);
+      if (e == s) continue;  // a rank without rows takes part in nothing
+      if (rank == root) {
+        ops[k++] = eegfx_gather_op{r == root ? EEGFX_GATHER_COPY : EEGFX_GATHER_RECV, r, s, e - s};
+      } else if (r == rank) {
+        ops[k++] = eegfx_gather_op{EEGFX_GATHER_SEND, root, s, e - s};
+      }
+    }
+    *n_ops = k;
+  });
+}
+
+int eegfx_gather_root(eegfx_comm* comm, const double* local, int64_t n_total, int64_t cols,
+                      int32_t root, double* out) {
+  return guarded([&] {
+    if (!comm || n_total < 0 || cols < 1) fail(EEGFX_EINVAL, "gather_root arguments");
+    if (root < 0 || root >= comm->world) fail(EEGFX_EINVAL, "root %d of %d", root, comm->world);
+    std::vector<eegfx_gather_op> ops((size_t)comm->world);
+    int32_t k = 0;
+    const int rc = eegfx_gather_root_plan(n_total, comm->world, comm->rank, root, ops.data(), &k);
+    if (rc != EEGFX_OK) fail(rc, "%s", last_error().c_str());
+    if (comm->rank == root && n_total > 0 && !out) fail(EEGFX_EINVAL, "null out on the root");
+    for (int i = 0; i < k; ++i)
+      if (ops[(size_t)i].kind != EEGFX_GATHER_RECV && !local) fail(EEGFX_EINVAL, "null local rows");
+    if (hipSetDevice(ctx_device(comm->ctx)) != hipSuccess)
+      fail(EEGFX_EHIP, "hipSetDevice(%d)", ctx_device(comm->ctx));
+    const hipStream_t st = (hipStream_t)ctx_stream(comm->ctx);
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    ncclResult_t r = ncclSuccess;
+    hipError_t h = hipSuccess;
+    for (int i = 0; i < k && r == ncclSuccess && h == hipSuccess; ++i) {
+      const eegfx_gather_op& op = ops[(size_t)i];
+      const size_t count = (size_t)(op.rows * cols);
+      if (op.kind == EEGFX_GATHER_SEND) {
+        r = ncclSend(local, count, ncclDouble, op.peer, comm->comm, st);
+      } else if (op.kind == EEGFX_GATHER_RECV) {
+        r = ncclRecv(out + op.row * cols, count, ncclDouble, op.peer, comm->comm, st);
+      } else if (local != out + op.row * cols) {  // the root's own rows
+        h = hipMemcpyAsync(out + op.row * cols, local, sizeof(double) * count,
+                           hipMemcpyDeviceToDevice, st);
+      }
+    }
+    const ncclResult_t g = ncclGroupEnd();
+    nccl_check(r, "ncclSend/ncclRecv");
+    if (h != hipSuccess) fail(EEGFX_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(h));
     nccl_check(g, "ncclGroupEnd");
   });
 }

@@ -5,10 +5,13 @@ OffLineDataProvider.java:248-260 carries across markers and files) every selecte
 independent, so ranks take contiguous ranges of the selected-epoch list and run the fused kernel on
 their range with no data-path collective.  The only exchange is moving the per-rank feature
 matrices to their consumers, in rank order, which is the reference's list order
-(``getData()`` order).  The product gather is :class:`Comm` over the C ABI (``eegfx_gather``: one
-RCCL broadcast per rank inside a group, ragged shards landing directly in their rows);
-:func:`gather_features` is the same exchange through ``torch.distributed`` (any backend -- gloo
-in the CPU tests), kept as the comparison leg of ``bench.py``.
+(``getData()`` order).  The product gathers are :class:`Comm` over the C ABI:
+``Comm.gather_root`` (``eegfx_gather_root``: the matrix on one rank -- the reference's single
+consumer, ``getData()`` in one JVM -- by grouped RCCL send/recv, ragged shards landing directly in
+their rows) and ``Comm.gather`` (``eegfx_gather``: the matrix on every rank, one RCCL broadcast
+per rank inside a group).  :func:`gather_features_root` / :func:`gather_features` are the same
+exchanges through ``torch.distributed`` (any backend -- gloo in the CPU tests), following the
+same plans; ``bench.py`` times them beside the C-ABI legs.
 """
 from __future__ import annotations
 
@@ -56,6 +59,43 @@ def gather_schedule(n_total: int, world: int):
     return [(int(o), int(c)) for o, c in zip(off, cnt)]
 
 
+def gather_root_plan(n_total: int, world: int, rank: int, root: int = 0):
+    """eegfx_gather_root_plan through the C ABI: the point-to-point operations eegfx_gather_root
+    issues on `rank`, as (kind, peer, first row, rows) with kind "send" / "recv" / "copy"."""
+    from ctypes import byref, c_int32
+    from ._lib import GatherOp, check, lib
+    ops = (GatherOp * max(1, world))()
+    k = c_int32()
+    check(lib().eegfx_gather_root_plan(n_total, world, rank, root, ops, byref(k)))
+    kinds = ("send", "recv", "copy")
+    return [(kinds[o.kind], int(o.peer), int(o.row), int(o.rows)) for o in ops[:k.value]]
+
+
+def gather_features_root(local, n_total: int, root: int = 0, group=None):
+    """The rooted gather through torch.distributed point-to-point ops, following
+    gather_root_plan: returns [n_total][F] on `root`, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    plan = gather_root_plan(n_total, world, rank, root)
+    feat = local.shape[1]
+    out = (torch.empty((n_total, feat), dtype=local.dtype, device=local.device)
+           if rank == root else None)
+    reqs = []
+    for kind, peer, row, rows in plan:
+        if kind == "send":
+            reqs.append(dist.isend(local.contiguous(), peer, group=group))
+        elif kind == "recv":
+            reqs.append(dist.irecv(out[row:row + rows], peer, group=group))
+        else:
+            out[row:row + rows] = local
+    for r in reqs:
+        r.wait()
+    return out
+
+
 def native_shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     """eegfx_shard_range through the C ABI (same partition as shard_range)."""
     from ctypes import byref, c_int64
@@ -70,8 +110,9 @@ class Comm:
 
     ``Comm.unique_id()`` on rank 0, shipped to the other ranks out of band, then
     ``Comm(ctx, world, rank, uid)`` on every rank; ``Comm.init_all(ctxs)`` for one process that
-    drives several devices.  ``gather(local, n_total)`` returns the [n_total][F] feature matrix in
-    rank order on every rank (device tensors, the context's stream)."""
+    drives several devices.  ``gather_root(local, n_total, root)`` returns the [n_total][F]
+    feature matrix in rank order on the root (None elsewhere); ``gather(local, n_total)`` returns
+    it on every rank (device tensors, the context's stream)."""
 
     ID_BYTES = 128
 
@@ -135,6 +176,36 @@ class Comm:
         local = local.contiguous()
         self.ctx._call(1, local, lib().eegfx_gather, self.handle,
                        local.data_ptr() if local.numel() else None, n_total, cols, out.data_ptr())
+        return out
+
+    def gather_root(self, local, n_total: int, root: int = 0, out=None):
+        """local: this rank's rows, as for gather(); returns [n_total][cols] on `root` (in
+        getData() order) and None on every other rank (eegfx_gather_root)."""
+        import torch
+        from ._lib import lib
+        rank, world = self.rank_world()
+        if not 0 <= root < world:
+            raise ValueError(f"root {root} outside world {world}")
+        s, e = shard_range(n_total, rank, world)
+        if local.dim() != 2 or local.dtype != torch.float64 or not local.is_cuda:
+            raise ValueError("local rows must be a 2-D float64 device tensor")
+        if local.shape[0] != e - s:
+            raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard of {n_total} "
+                             f"over {world} ranks is [{s}, {e})")
+        cols = int(local.shape[1])
+        if rank == root:
+            if out is None:
+                out = torch.empty((n_total, cols), dtype=torch.float64, device=local.device)
+            elif (tuple(out.shape) != (n_total, cols) or out.dtype != torch.float64
+                  or not out.is_contiguous()):
+                raise ValueError(f"out must be a contiguous float64 tensor of shape "
+                                 f"({n_total}, {cols})")
+        else:
+            out = None
+        local = local.contiguous()
+        self.ctx._call(1, local, lib().eegfx_gather_root, self.handle,
+                       local.data_ptr() if local.numel() else None, n_total, cols, root,
+                       out.data_ptr() if out is not None and out.numel() else None)
         return out
 
     def close(self) -> None:

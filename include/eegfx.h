@@ -269,6 +269,31 @@ int eegfx_comm_init_all(eegfx_ctx* const* ctxs, int32_t n, eegfx_comm** out /* n
 int eegfx_comm_rank(const eegfx_comm* comm, int32_t* rank, int32_t* world);
 int eegfx_gather(eegfx_comm* comm, const double* local, int64_t n_total, int64_t cols,
                  double* out);
+/* Rooted gather ("grouped ncclSend/ncclRecv to rank 0"): the [n_total][cols]
+ * matrix is assembled on `root` only -- the reference's consumer is one JVM holding one list
+ * (OffLineDataProvider.java:370-379 getData(), parallelize on the driver in
+ * LogisticRegressionClassifier.java:87-94).  Every other rank sends its shard once, the root
+ * receives each ragged shard straight into its rows of `out` (its own shard: a device copy, or
+ * nothing when `local` already is those rows), all inside one RCCL group, on the context
+ * stream.  `out` is read on the root only (may be NULL elsewhere).  Root inbound traffic is
+ * (world-1)/world of the matrix over its world-1 xGMI links, where eegfx_gather moves the whole
+ * matrix to every rank. */
+int eegfx_gather_root(eegfx_comm* comm, const double* local, int64_t n_total, int64_t cols,
+                      int32_t root, double* out);
+/* The point-to-point plan eegfx_gather_root issues on `rank` (pure host function): up to `world`
+ * operations {kind, peer, first row, rows}; the root receives from every other rank with rows
+ * (in rank order) and copies its own shard, every other rank with rows sends once to the root. */
+#define EEGFX_GATHER_SEND 0
+#define EEGFX_GATHER_RECV 1
+#define EEGFX_GATHER_COPY 2
+typedef struct {
+  int32_t kind;  /* EEGFX_GATHER_SEND | _RECV | _COPY                          */
+  int32_t peer;  /* the other rank (the root for a send; the rank itself for a copy) */
+  int64_t row;   /* first row of the shard in the [n_total][cols] matrix             */
+  int64_t rows;  /* rows moved                                                        */
+} eegfx_gather_op;
+int eegfx_gather_root_plan(int64_t n_total, int32_t world, int32_t rank, int32_t root,
+                           eegfx_gather_op* ops /* world entries */, int32_t* n_ops);
 int eegfx_group_start(void);
 int eegfx_group_end(void);
 int eegfx_comm_destroy(eegfx_comm* comm);

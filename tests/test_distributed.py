@@ -54,6 +54,37 @@ def test_gather_schedule_matches_shard_range():
         gather_schedule(-1, 2)
 
 
+def test_gather_root_plan_matches_shard_range():
+    """eegfx_gather_root_plan (the send/recv plan of the rooted gather) for ragged n over 1..8
+    ranks and every root: the root receives each other rank's shard_range rows once, in rank
+    order, and copies its own; every other rank with rows sends exactly its shard to the root;
+    ranks without rows issue nothing; the root's operations tile [0, n) in getData() order."""
+    import eeg_dataanalysispackage_amd as fx
+    from eeg_dataanalysispackage_amd.sharding import gather_root_plan
+    for n in (0, 1, 5, 7, 8, 9, 63, 64, 65, 1_000_003, 64_000_000, 64_000_007):
+        for world in range(1, 9):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            for root in range(world):
+                plans = [gather_root_plan(n, world, r, root) for r in range(world)]
+                got = plans[root]
+                want = [("copy" if r == root else "recv", r, s, e - s)
+                        for r, (s, e) in enumerate(spans) if e > s]
+                assert got == want, (n, world, root)
+                assert sum(op[3] for op in got) == n
+                assert all(a[2] + a[3] == b[2] for a, b in zip(got, got[1:]))
+                for r in range(world):
+                    if r == root:
+                        continue
+                    s, e = spans[r]
+                    assert plans[r] == ([("send", root, s, e - s)] if e > s else []), (n, world, r)
+    with pytest.raises(fx.EegfxError):
+        gather_root_plan(10, 2, 2, 0)
+    with pytest.raises(fx.EegfxError):
+        gather_root_plan(10, 2, 0, 2)
+    with pytest.raises(fx.EegfxError):
+        gather_root_plan(-1, 2, 0, 0)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -110,6 +141,45 @@ def _schedule_worker(rank, world, port, n, out_dir):
     np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([torch.equal(out, full_ref)]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _root_worker(rank, world, port, n, root, out_dir):
+    """eegfx_gather_root's pattern rehearsed on gloo (gather_features_root follows
+    eegfx_gather_root_plan): extraction on each rank's shard (the oracle stands in for the kernels
+    here), the matrix assembled on the root only, equal to the single-process matrix bit for bit
+    in getData() order (OffLineDataProvider.java:370-372)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eeg_dataanalysispackage_amd.sharding import gather_features_root
+    from oracle import oracle
+    rng = np.random.default_rng(321)
+    nf = 1000 * n + 2000
+    raw = (rng.integers(-26000, -24000, size=(1, 3)) +
+           np.cumsum(rng.integers(-40, 41, size=(nf, 3)), axis=0)).astype(np.int16)
+    pos = np.arange(1000, 1000 * (n + 1), 1000)
+    s, e = shard_range(n, rank, world)
+    local = torch.from_numpy(oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos[s:e])
+                             .reshape(e - s, 48))
+    full = gather_features_root(local, n, root)
+    if rank == root:
+        ref = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
+        ok = np.array_equal(full.numpy(), ref)
+    else:
+        ok = full is None
+    np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([ok]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,root", [(2, 37, 0), (3, 7, 2), (4, 2, 1), (4, 9, 0)])
+def test_gather_root_send_recv_world_n(tmp_path, world, n, root):
+    import torch.multiprocessing as mp
+    mp.spawn(_root_worker, args=(world, _free_port(), n, root, str(tmp_path)), nprocs=world,
+             join=True)
+    assert all(bool(np.load(tmp_path / f"ok{r}.npy")[0]) for r in range(world))
 
 
 @pytest.mark.parametrize("world,n", [(3, 7), (4, 2), (2, 37)])

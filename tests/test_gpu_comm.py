@@ -67,6 +67,28 @@ def test_gather_after_fused_path(ctx):
     comm.close()
 
 
+def test_single_rank_gather_root(ctx):
+    """eegfx_gather_root at world 1: the root's own shard is copied (or left in place when
+    `local` already is the output rows); `out` comes back on the root."""
+    comm = Comm(ctx, 1, 0, Comm.unique_id())
+    local = _rows(999, 5)
+    torch.cuda.synchronize()
+    out = comm.gather_root(local, 999, root=0)
+    ctx.synchronize()
+    assert torch.equal(out, local) and out.data_ptr() != local.data_ptr()
+    same = comm.gather_root(local, 999, root=0, out=local)  # in place: no copy issued
+    ctx.synchronize()
+    assert same.data_ptr() == local.data_ptr() and torch.equal(same, out)
+    empty = comm.gather_root(_rows(0, 6), 0)
+    ctx.synchronize()
+    assert tuple(empty.shape) == (0, 48)
+    with pytest.raises(ValueError):
+        comm.gather_root(local, 999, root=1)
+    with pytest.raises(fx.EegfxError):
+        check(fx.lib().eegfx_gather_root(comm.handle, local.data_ptr(), 999, 48, 0, None))
+    comm.close()
+
+
 def test_gather_errors(ctx):
     comm = Comm(ctx, 1, 0, Comm.unique_id())
     with pytest.raises(fx.EegfxError):

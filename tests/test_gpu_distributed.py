@@ -34,7 +34,7 @@ def _recording(n):
     return raw, pos
 
 
-def _rank(rank, world, port, n, numerics, out_dir):
+def _rank(rank, world, port, n, numerics, out_dir, mode="broadcast"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -50,6 +50,16 @@ def _rank(rank, world, port, n, numerics, out_dir):
     local = ctx.process_recording(d_raw, 3, [0, 1, 2], [0.1] * 3, d_pos)  # device rows
     local = local.cpu()
     ctx.close()
+    if mode == "root":  # eegfx_gather_root's send/recv plan, assembled on the last rank
+        from eeg_dataanalysispackage_amd.sharding import gather_features_root
+        full = gather_features_root(local, n, world - 1)
+        if rank == world - 1:
+            np.save(os.path.join(out_dir, "rows_root.npy"), full.numpy())
+        else:
+            assert full is None
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     out = torch.full((n, 48), float("nan"), dtype=torch.float64)
     for root, (off, cnt) in enumerate(gather_schedule(n, world)):
         if cnt == 0:
@@ -77,3 +87,20 @@ def test_device_shards_assemble_in_getdata_order(tmp_path, world, n, numerics):
             assert np.array_equal(got, want), f"rank {r}"
         else:
             assert np.max(np.abs(got - want)) <= 1e-9, f"rank {r}"
+
+
+@pytest.mark.parametrize("world,n,numerics", [(3, 64, "exact"), (2, 11, "fma")])
+def test_device_shards_gathered_on_root_in_getdata_order(tmp_path, world, n, numerics):
+    """The rooted plan (eegfx_gather_root_plan): only the root holds the matrix, equal to the
+    oracle over the whole recording in getData() order."""
+    import torch.multiprocessing as mp
+    from oracle import oracle
+    mp.spawn(_rank, args=(world, _free_port(), n, numerics, str(tmp_path), "root"), nprocs=world,
+             join=True)
+    raw, pos = _recording(n)
+    want = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
+    got = np.load(tmp_path / "rows_root.npy")
+    if numerics == "exact":
+        assert np.array_equal(got, want)
+    else:
+        assert np.max(np.abs(got - want)) <= 1e-9
