@@ -31,6 +31,14 @@
 
 #include <cstdint>
 
+#include "dwt8_taps.h"
+
+// FMA numerics' filter bank: levels 1-5 collapsed into one 280-tap filter (dwt8_collapsed_cascade)
+// or the level-by-level cascade with partial-sum halos (dwt8_fast_cascade; A/B builds only).
+#ifndef EEGFX_COLLAPSED
+#define EEGFX_COLLAPSED 1
+#endif
+
 namespace eegfx {
 namespace dev {
 
@@ -352,6 +360,56 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
   double a1[40];
   level1_ps(fetch, r, b, gbase, s, a1);
   levels2to6_ps(a1, gbase, s, a6, d6);
+}
+
+// Levels 1-5 collapsed (fma numerics): a5[k] = sum_{m < 280} H5[m] x[32 k + m] (mod 512), the five
+// periodic low-pass stages composed into one filter at stride 32 (dwt8_taps.h, generated exactly by
+// gen_taps.py).  4,480 multiply-adds per signal for a5 instead of the cascade's 4,960, and the
+// cross-lane traffic shrinks to one partial-sum round: lane s owns a5[2s], a5[2s+1]; its sample
+// n (and n + 32) meets taps H5[n + 32 j] of the outputs of lanes s, s-1, ..., s-4, so it keeps ten
+// partial sums P[j], j = -1..8 (the partial of a5[2(s - d) + i] with j = 2d - i), and receives the
+// other four terms of each of its two outputs from lanes s+1..s+4 (8 doubles instead of the
+// cascade's 16 halo partials over levels 1-5).  Level 6 (a6, d6 from a5) is unchanged.  The
+// samples are taken in pairs (n, n + 32), which meet the same nine taps: one 80-byte scalar load
+// per pair, the taps held in SGPRs.  Only the summation order differs from the reference's, inside
+// the 1e-9 contract; EXACT keeps the level-by-level cascade.
+static __constant__ double kH5[kH5Rows * kH5Cols] = EEGFX_H5_TABLE;
+
+template <typename Fetch>
+__device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
+                                                       int s, double& a6, double& d6) {
+  typedef const __attribute__((address_space(4))) double* const_f64_ptr;
+  const_f64_ptr tab = (const_f64_ptr)kH5;
+  asm volatile("" : "+s"(tab));  // scalar loads of the table, not per-tap literal moves
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  double P[10];  // P[j + 1]
+#pragma unroll
+  for (int n = 0; n < 32; ++n) {
+    const dwt8_f32x2 v = {fetch(n), fetch(n + 32)};
+    const dwt8_f32x2 y = v * rr - bb;
+    const double x0 = (double)y.x, x1 = (double)y.y;
+    const const_f64_ptr T = tab + n * kH5Cols;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if (n + 32 * j >= 280) continue;
+      const double t = T[j];
+      P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
+      if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
+      else P[j] = __builtin_fma(x1, t, P[j]);
+    }
+  }
+  double a5[2 + 8];
+  a5[0] = P[1];
+  a5[1] = P[0];
+#pragma unroll
+  for (int d = 1; d <= 4; ++d) {
+    const int src = gbase + ((s + d) & (kLanesPerSignal - 1));
+    a5[0] += __shfl(P[2 * d + 1], src, 64);
+    a5[1] += __shfl(P[2 * d], src, 64);
+  }
+  halo<2, true>(a5, nullptr, gbase, s);
+  a6 = fir10<true, false>(a5);
+  d6 = fir10<true, true>(a5);
 }
 
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps

@@ -208,8 +208,13 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
     double a6, d6;
     if constexpr (FAST) {  // the 8 lanes of a group share the signal: partial-sum halos
+#if EEGFX_COLLAPSED
+      dwt8_collapsed_cascade([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
+                             a6, d6);
+#else
       dwt8_fast_cascade([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
                         a6, d6);
+#endif
     } else {
       double a1[40];
       (void)nxt;
@@ -322,8 +327,13 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   const float b = base[e * C + c];
   double a6, d6;
   if constexpr (FAST) {
+#if EEGFX_COLLAPSED
+    dwt8_collapsed_cascade([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7,
+                           s, a6, d6);
+#else
     dwt8_fast_cascade([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7, s,
                       a6, d6);
+#endif
   } else {
     double a1[40];
     (void)nxt;
