@@ -26,6 +26,9 @@
 // following lanes sum the taps that fall on their slices; dwt8_fast_cascade / levels2to6_ps), so
 // the boundary outputs add their taps in two or three chains; within 1e-9 of EXACT, tested.
 #pragma once
+// classic guard as well: a perf-probe build may include a patched copy of this header first
+#ifndef EEGFX_DWT8_H
+#define EEGFX_DWT8_H
 
 #include <hip/hip_runtime.h>
 
@@ -454,3 +457,5 @@ __device__ __forceinline__ void dwt8_cascade(const double (&x)[kIn], double* xch
 
 }  // namespace dev
 }  // namespace eegfx
+
+#endif  // EEGFX_DWT8_H

@@ -31,7 +31,8 @@
 //
 // The alternatives measured against this pair (persistent, work-queue, two-sub-tile and
 // loader/consumer variants, the baselines folded into the window kernel, the collapsed operator
-// on the FP64 matrix cores) are kept under tools/probes/rejected/ with their numbers in
+// on the FP64 matrix cores, the register-direct window) are kept as patches under
+// tools/probes/history/ with their numbers in
 // DESIGN.md §6; none of them ships.
 #include <hip/hip_runtime.h>
 

@@ -91,7 +91,7 @@ def test_plain_c_consumer(tmp_path):
 
 def test_no_environment_knobs_in_the_product():
     """The kernel choice of every call is a function of its arguments only: no getenv in the
-    library sources (the rejected perf-study variants live under tools/probes/rejected/)."""
+    library sources (the rejected perf-study variants live as patches under tools/probes/history/)."""
     csrc = os.path.join(REPO, "eeg_dataanalysispackage_amd", "csrc")
     for f in os.listdir(csrc):
         if f.endswith((".hip", ".cpp", ".h")):

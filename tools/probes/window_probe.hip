@@ -1,12 +1,12 @@
 // Probe: window_kernel (the fused c3 path) or window_wide_kernel (configs[3]) timed under sustained
 // load, for A/B studies of kernel variants.  FUSED_SRC / WIDE_SRC name the kernel source to build
-// against (default: the product files); a variant is a modified copy under tools/probes/variants/.
+// against (default: the product files); build_probes.sh builds one per tools/probes/ablations/ patch.
 //
-//   hipcc ... -DFUSED_SRC='"variants/v1/fused.hip"' window_probe.hip -o window_probe_v1
+//   hipcc ... -DFUSED_SRC='"build/v1/fused.hip"' window_probe.hip -o window_probe_v1
 //   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
 //
 // Phase timestamps (per-workgroup s_memrealtime at each phase boundary):
-//   hipcc ... -DFUSED_SRC='"rejected/phase_timestamps/fused.hip"' -DPROBE_TIMESTAMPS ...
+//   restore_variant.sh phase_timestamps_fused, then -DFUSED_SRC='"<dir>/fused.hip"' -DPROBE_TIMESTAMPS
 //
 // Inputs are the bench workload: synth_kernel recording (configs[1]: 1M epochs x 3 ch, or
 // configs[3]: 250k epochs x 32 ch), one marker every 1,000 frames.  Prints the average launch time
@@ -72,7 +72,7 @@ int main() {
   float ms;
   (void)hipEventElapsedTime(&ms, a, b);
 #ifdef PROBE_TIMESTAMPS
-  {  // one more launch with per-workgroup phase timestamps (variants/ts)
+  {  // one more launch with per-workgroup phase timestamps
     const size_t nwg = (size_t)((n + 7) / 8);
     unsigned long long* d_ts;
     (void)hipMalloc(&d_ts, nwg * 5 * 8);
