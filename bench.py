@@ -41,7 +41,10 @@ def bytes_per_epoch(ct, C):
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFS = 78.6                    # vendor fp64 vector spec (not in the guide)
 FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01/r01b_perf_study.json)
-FLOP_PER_SIGNAL = 2 * 5120                     # minimal a-path cascade, per channel
+# fp64 filter-bank flops per channel: fma numerics run levels 1-5 as the collapsed 280-tap filter
+# (16 x 280 + level 6's 16 x 10 = 4,640 MAC, dwt8.h), EXACT the level-by-level a-path cascade
+# (5,120 MAC)
+FLOP_PER_SIGNAL = {"fma": 2 * 4640, "exact": 2 * 5120}
 FRAMES_PER_EPOCH = 1000                        # one marker per second at 1000 Hz
 SEED = 0x5EED
 WINDOW_KERNEL = "window_kernel<int16,3>"
@@ -118,13 +121,14 @@ def traffic_from_profiles(workload_key):
     return best
 
 
-CEILING_FILE = os.path.join("profiles", "r02_ceiling.json")
+CEILING_FILE = os.path.join("profiles", "r03_ceiling.json")
 
 
 def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
-    """The attainable bound of the dominant kernel (profiles/r02_ceiling.json): its VALU issue
-    time at the clock the chip holds under the kernel's own sustained power draw (SQ counters +
-    amd-smi under load), scaled to this launch's epochs, next to the live kernel time."""
+    """The attainable bound of the dominant kernel (profiles/r03_ceiling.json, written by
+    tools/ceiling_summary.py): its VALU issue time at the clock the chip holds under the kernel's
+    own sustained power draw (SQ counters + amd-smi under load), scaled to this launch's epochs,
+    next to the live kernel time."""
     if numerics != "fma":
         return None
     key = {3: "window_kernel<int16,3> fma", 32: "window_c32_kernel fma"}.get(C)
@@ -140,6 +144,24 @@ def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
             "valu_instr_per_wave": k["valu_instr_per_wave"],
             "clock_MHz_under_load": k["clock_MHz_under_load"],
             "source": CEILING_FILE}
+
+
+def whole_path_ceiling(C, numerics, n, step_ms, bpe):
+    """The attainable bound of the whole c3 step: baseline_kernel at its own measured time (it
+    runs below the power cap, bound by its memory pattern) plus the window kernel's VALU bound,
+    scaled to this launch's epochs (profiles/r03_ceiling.json)."""
+    if numerics != "fma" or C != 3:
+        return None
+    try:
+        d = json.load(open(os.path.join(REPO, CEILING_FILE)))
+        b = d["baseline_kernel<int16,3>"]["ms_alone"]
+        w = d["kernels"]["window_kernel<int16,3> fma"]
+    except Exception:
+        return None
+    ms = (b + w["ceiling_ms"]) * n / w["epochs_per_launch"]
+    return {"ms": round(ms, 4), "frac": round(n * bpe / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_over_ceiling": round(ms / step_ms, 4),
+            "baseline_kernel_ms_alone": b, "source": CEILING_FILE}
 
 
 _JSON_OUT = None
@@ -337,16 +359,18 @@ def main():
                 "traffic_source": (prof.get("source") if prof else None),
                 "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": bpe,
                                "GBps": round(path_gbs, 1),
-                               "frac": round(path_gbs / HBM_PEAK_GBS, 4)},
+                               "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                               "ceiling": whole_path_ceiling(C, args.numerics, n, step_ms, bpe)},
                 # the other side of the kernel's balance: fp64 filter-bank flops
                 # (5,120 MAC per signal) against the vector fp64 peak, and the VALU issue share
                 # of the kernel's cycles from the committed SQ counter pass
-                "fp64": {"flop_per_epoch": FLOP_PER_SIGNAL * C,
-                         "achieved_TFs": round(FLOP_PER_SIGNAL * C * n / (kernel_ms * 1e-3) / 1e12, 2),
+                "fp64": {"flop_per_epoch": FLOP_PER_SIGNAL[args.numerics] * C,
+                         "achieved_TFs": round(FLOP_PER_SIGNAL[args.numerics] * C * n
+                                               / (kernel_ms * 1e-3) / 1e12, 2),
                          "peak_TFs": FP64_VECTOR_PEAK_TFS,
                          "measured_fma_peak_TFs": FP64_FMA_MEASURED_TFS,
-                         "frac": round(FLOP_PER_SIGNAL * C * n / (kernel_ms * 1e-3) / 1e12
-                                       / FP64_VECTOR_PEAK_TFS, 4)},
+                         "frac": round(FLOP_PER_SIGNAL[args.numerics] * C * n / (kernel_ms * 1e-3)
+                                       / 1e12 / FP64_VECTOR_PEAK_TFS, 4)},
                 "ceiling": ceiling_from_profiles(C, args.numerics, n, kernel_ms, kernel_bytes),
             },
             "cpu_baseline": cpu,

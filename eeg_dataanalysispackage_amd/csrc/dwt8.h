@@ -378,7 +378,10 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // the 1e-9 contract; EXACT keeps the level-by-level cascade.
 static __constant__ double kH5[kH5Rows * kH5Cols] = EEGFX_H5_TABLE;
 
-template <typename Fetch>
+// REGION: one scheduling region per sample pair (c3 window kernel: the compiler otherwise hoists
+// the tap rows into SGPRs it then spills to VGPR lanes; 870 -> 854 VALU per wave, -0.7 %; the c32
+// kernel, with fewer waves to cover the exposed scalar-load latency, measured +0.4 % with it).
+template <bool REGION = false, typename Fetch>
 __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
                                                        int s, double& a6, double& d6) {
   typedef const __attribute__((address_space(4))) double* const_f64_ptr;
@@ -400,6 +403,7 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
       if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
       else P[j] = __builtin_fma(x1, t, P[j]);
     }
+    if constexpr (REGION) __builtin_amdgcn_sched_barrier(0);
   }
   double a5[2 + 8];
   a5[0] = P[1];

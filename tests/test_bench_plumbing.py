@@ -13,7 +13,10 @@ from conftest import REPO
 def test_algorithmic_bytes_per_epoch():
     assert bench.bytes_per_epoch(3, 3) == 4064
     assert bench.bytes_per_epoch(32, 32) == 43272     # configs[3]
-    assert bench.FLOP_PER_SIGNAL * 3 == 30720
+    # fma: levels 1-5 as the collapsed 280-tap filter (16 x 280 + 16 x 10 MAC per channel);
+    # EXACT: the a-path cascade (5,120 MAC per channel)
+    assert bench.FLOP_PER_SIGNAL["fma"] == 2 * (16 * 280 + 16 * 10)
+    assert bench.FLOP_PER_SIGNAL["exact"] * 3 == 30720
 
 
 def test_traffic_reader_takes_the_newest_summary():
@@ -38,3 +41,15 @@ def test_ceiling_reader_scales_to_the_launch():
     assert 0.5 < c["frac"] < 0.8            # the measured power-capped bound, not HBM's 1.0
     assert bench.ceiling_from_profiles(3, "exact", 1, 1.0, 1) is None
     assert bench.ceiling_from_profiles(7, "fma", 1, 1.0, 1) is None
+
+
+def test_whole_path_ceiling_adds_the_baseline_pass():
+    d = json.load(open(os.path.join(REPO, bench.CEILING_FILE)))
+    b = d["baseline_kernel<int16,3>"]["ms_alone"]
+    w = d["kernels"]["window_kernel<int16,3> fma"]["ceiling_ms"]
+    c = bench.whole_path_ceiling(3, "fma", 1_000_000, 1.0, 4064)
+    assert c["ms"] == pytest.approx(b + w, abs=1e-4)
+    assert c["frac"] == pytest.approx(4.064e9 / ((b + w) * 1e-3) / 8e12, rel=1e-3)
+    assert 0.5 < c["frac"] < 0.8
+    assert bench.whole_path_ceiling(32, "fma", 1, 1.0, 1) is None
+    assert bench.whole_path_ceiling(3, "exact", 1, 1.0, 1) is None

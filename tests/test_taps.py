@@ -68,3 +68,11 @@ def test_lane_algebra_matches_the_cascade():
             a = np.array([sum(h[t] * a[(2 * k + t) % N] for t in range(10)) for k in range(N // 2)])
         got = _lane_model(x, tab)
         assert np.max(np.abs(got - a)) <= 1e-12 * np.max(np.abs(a))
+
+
+def test_literals_are_the_kernel_taps():
+    import re
+    with open(os.path.join(CSRC, "dwt8.h")) as f:
+        src = f.read()
+    got = [re.search(r"#define EEGFX_H%d (\S+)" % j, src).group(1) for j in range(10)]
+    assert got == gen_taps.H_LITERALS

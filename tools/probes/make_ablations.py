@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Regenerates tools/probes/ablations/*.patch against the current product sources.
+
+Each ablation is a list of exact text replacements in fused.hip / wide.hip / dwt8.h.  When the
+product changes, rerun this script; a replacement whose text no longer exists fails loudly.
+build_probes.sh applies the patches to copies of the sources and builds window_probe_<name>;
+tools/ablation_study.sh measures them.
+
+  python3 tools/probes/make_ablations.py
+"""
+import difflib
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "..", "..", "eeg_dataanalysispackage_amd", "csrc")
+FILES = ("fused.hip", "wide.hip", "dwt8.h")
+
+DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  dma_drain();"""
+
+FMA_BODY = """#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if (n + 32 * j >= 280) continue;
+      const double t = T[j];
+      P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
+      if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
+      else P[j] = __builtin_fma(x1, t, P[j]);
+    }"""
+
+ABLATIONS = {
+    "cascade": (
+        "fma filter bank as the round-2 level-by-level cascade with partial-sum halos "
+        "(A/B against the collapsed filter)",
+        [("dwt8.h", "#define EEGFX_COLLAPSED 1", "#define EEGFX_COLLAPSED 0")]),
+    "nodma": (
+        "no window DMA: removes the HBM window reads and the LDS writes; LDS reads, decode and "
+        "fp64 kept (wrong results)",
+        [("fused.hip", DMA_ISSUE,
+          "  (void)rows;  // ablation: no window DMA (no HBM window reads, no LDS writes)")]),
+    "l2src": (
+        "window DMA from a 2 MB L2-resident region (same addresses mod 2 MB): removes HBM reads "
+        "only (wrong results)",
+        [("fused.hip", "    const uint8_t* sb = raw + Bq;",
+          "    const uint8_t* sb = raw + (Bq & 0x1FFFF0);  // ablation: L2-resident source")]),
+    "regdirect": (
+        "no LDS staging: each lane loads its 64 samples (128 B, L2-resident region) into VGPRs; "
+        "no window DMA, no LDS sample reads (wrong results)",
+        [("fused.hip", DMA_ISSUE,
+          "  (void)rows;  // ablation: no LDS staging; the lane's 64 samples come from VGPRs"),
+         ("fused.hip", """  double a6, d6;
+  cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);""",
+          """  double a6, d6;
+  (void)own; (void)nxt;
+  u32x4_a4 q[8];
+  {
+    const int64_t wv = mine ? wb[e0 + el] : 0;
+    const u32x4_a16* src = (const u32x4_a16*)(raw + ((wv + 384 * s + 128 * w) & 0x1FFFF0));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = src[i];
+  }
+  dwt8_collapsed_cascade<true>([&](int k) {
+    const uint32_t v = q[k >> 3][(k >> 1) & 3];
+    return (float)(int16_t)((k & 1) ? (v >> 16) : (v & 0xffffu));
+  }, r, b, lane & ~7, s, a6, d6);""")]),
+    "nofp64": (
+        "fp64 filter bank removed: the 560 FMAs per lane become 64 fp64 adds; DMA, LDS reads and "
+        "decode kept (wrong results)",
+        [("dwt8.h", FMA_BODY, """    (void)T;  // ablation: no fp64 filter work, the decoded samples are summed
+    if (n < 10) { P[n] = x0 + x1; } else { P[n % 10] += x0; P[(n + 5) % 10] += x1; }""")]),
+}
+
+
+def main():
+    src = {f: open(os.path.join(CSRC, f)).read() for f in FILES}
+    out_dir = os.path.join(HERE, "ablations")
+    os.makedirs(out_dir, exist_ok=True)
+    for old in os.listdir(out_dir):
+        if old.endswith(".patch"):
+            os.remove(os.path.join(out_dir, old))
+    for name, (what, edits) in ABLATIONS.items():
+        new = dict(src)
+        for f, a, b in edits:
+            if a not in new[f]:
+                sys.exit(f"ablation {name}: text not found in {f}:\n{a}")
+            new[f] = new[f].replace(a, b, 1)
+        lines = [f"# ablation: {what}\n"]
+        for f in FILES:
+            if new[f] != src[f]:
+                lines += difflib.unified_diff(src[f].splitlines(True), new[f].splitlines(True),
+                                              f"a/{f}", f"b/{f}")
+        with open(os.path.join(out_dir, name + ".patch"), "w") as fh:
+            fh.writelines(lines)
+        print(name)
+
+
+if __name__ == "__main__":
+    main()
