@@ -373,10 +373,10 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // partial sums P[j], j = -1..8 (the partial of a5[2(s - d) + i] with j = 2d - i), and receives the
 // other four terms of each of its two outputs from lanes s+1..s+4 (8 doubles instead of the
 // cascade's 16 halo partials over levels 1-5).  Level 6 (a6, d6 from a5) is unchanged.  The
-// samples are taken in pairs (n, n + 32), which meet the same nine taps: one 80-byte scalar load
-// per pair, the taps held in SGPRs.  Only the summation order differs from the reference's, inside
+// samples are taken in pairs (n, n + 32), which meet the same nine taps: one 64-byte scalar load
+// per pair plus the ninth from the table's tail, the taps held in SGPRs.  Only the summation order differs from the reference's, inside
 // the 1e-9 contract; EXACT keeps the level-by-level cascade.
-static __constant__ double kH5[kH5Rows * kH5Cols] = EEGFX_H5_TABLE;
+static __constant__ double kH5[kH5Tail + kH5Rows] = EEGFX_H5_TABLE;
 
 // REGION: one scheduling region per sample pair (c3 window kernel: the compiler otherwise hoists
 // the tap rows into SGPRs it then spills to VGPR lanes; 870 -> 854 VALU per wave, -0.7 %; the c32
@@ -398,7 +398,7 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       if (n + 32 * j >= 280) continue;
-      const double t = T[j];
+      const double t = j < kH5Cols ? T[j] : tab[kH5Tail + n];
       P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
       if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
       else P[j] = __builtin_fma(x1, t, P[j]);

@@ -30,12 +30,13 @@ def test_table_is_the_rounded_exact_composition():
     h = [Fraction(v) for v in gen_taps.H_LITERALS]
     # the composition is the polyphase product of the five stages: its sum is sum(h)^5
     assert sum(H) == sum(h) ** 5
-    tab = gen_taps.table()
     for n in range(32):
-        for j in range(10):
+        for j in range(9):
             m = n + 32 * j
-            want = float(H[m]) if j < 9 and m < 280 else 0.0
-            assert tab[n][j] == want
+            assert gen_taps.tap(n, j) == (float(H[m]) if m < 280 else 0.0)
+    rows, tail = gen_taps.table()
+    assert len(rows) == 32 and all(len(r) == 8 for r in rows) and len(tail) == 32
+    assert tail[24:] == (0.0,) * 8
 
 
 def _lane_model(x, tab):
@@ -47,8 +48,8 @@ def _lane_model(x, tab):
             for j in range(9):
                 if n + 32 * j >= 280:
                     continue
-                P[s][j + 1] = P[s][j + 1] + xs[n] * tab[n][j]
-                P[s][j] = P[s][j] + xs[n + 32] * tab[n][j]
+                P[s][j + 1] = P[s][j + 1] + xs[n] * tab(n, j)
+                P[s][j] = P[s][j] + xs[n + 32] * tab(n, j)
     a5 = np.zeros(16)
     for s in range(8):
         a5[2 * s] = P[s][1] + sum(P[(s + d) % 8][2 * d + 1] for d in range(1, 5))
@@ -58,7 +59,7 @@ def _lane_model(x, tab):
 
 def test_lane_algebra_matches_the_cascade():
     h = np.array([float(v) for v in gen_taps.H_LITERALS])
-    tab = np.array(gen_taps.table())
+    tab = gen_taps.tap
     rng = np.random.default_rng(7)
     for _ in range(4):
         x = rng.normal(size=512) * 300.0 + rng.normal() * 1000.0

@@ -23,7 +23,7 @@ DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane,
 FMA_BODY = """#pragma unroll
     for (int j = 0; j < 9; ++j) {
       if (n + 32 * j >= 280) continue;
-      const double t = T[j];
+      const double t = j < kH5Cols ? T[j] : tab[kH5Tail + n];
       P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
       if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
       else P[j] = __builtin_fma(x1, t, P[j]);
