@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "common.h"
+#include "eegfx_ext.h"
 #include "launch.h"
 
 using namespace eegfx;
