@@ -374,13 +374,14 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // other four terms of each of its two outputs from lanes s+1..s+4 (8 doubles instead of the
 // cascade's 16 halo partials over levels 1-5).  Level 6 (a6, d6 from a5) is unchanged.  The
 // samples are taken in pairs (n, n + 32), which meet the same nine taps: one 64-byte scalar load
-// per pair plus the ninth from the table's tail, the taps held in SGPRs.  Only the summation order differs from the reference's, inside
-// the 1e-9 contract; EXACT keeps the level-by-level cascade.
+// per pair plus the ninth from the table's tail, the taps held in SGPRs.  Only the summation order
+// differs from the reference's, inside the 1e-9 contract; EXACT keeps the level-by-level cascade.
 static __constant__ double kH5[kH5Tail + kH5Rows] = EEGFX_H5_TABLE;
 
-// REGION: one scheduling region per sample pair (c3 window kernel: the compiler otherwise hoists
-// the tap rows into SGPRs it then spills to VGPR lanes; 870 -> 854 VALU per wave, -0.7 %; the c32
-// kernel, with fewer waves to cover the exposed scalar-load latency, measured +0.4 % with it).
+// REGION: one scheduling region per sample pair.  In the c3 window kernel the compiler otherwise
+// hoists tap rows into SGPRs and spills them to VGPR lanes (870 -> 854 VALU per wave, -0.7 %); the
+// c32 kernel does not spill without it, and measured +0.4 % with it (more exposed scalar-load
+// latency), so it leaves it off.
 template <bool REGION = false, typename Fetch>
 __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
                                                        int s, double& a6, double& d6) {
