@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -98,15 +99,20 @@ int main() {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const char* names[6] = {"valu fma_f64", "mfma_f64_16x16x4", "split valu|mfma waves", "interleaved", "valu add_f64", "valu mul_f64"};
+  // PROBE_MODE=m: run mode m back to back for PROBE_LAUNCHES launches (socket power / clock
+  // sampled from outside, tools/fp64_energy.sh), then report its rate like the sweep below
+  const int only = getenv("PROBE_MODE") ? atoi(getenv("PROBE_MODE")) : -1;
+  const int reps = getenv("PROBE_LAUNCHES") ? atoi(getenv("PROBE_LAUNCHES")) : 5;
   for (int mode = 0; mode < 6; ++mode) {
+    if (only >= 0 && mode != only) continue;
     hipLaunchKernelGGL(probe, grid, block, 0, 0, mode, out, kIters);
     (void)hipEventRecord(a);
-    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(probe, grid, block, 0, 0, mode, out, kIters);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(probe, grid, block, 0, 0, mode, out, kIters);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
-    ms /= 5;
+    ms /= reps;
     const double waves = (double)grid.x * 8;
     // per wave-iteration: VALU 8 x 64 FMA, MFMA 4 x 1024 FMA
     double valu_fma = 0, mfma_fma = 0;
