@@ -32,8 +32,12 @@ namespace dev {
 // H5[32 (4 j0i + c) + 4 p0i + k], zero for tap blocks past 8 or taps past 279
 __constant__ double kB44[16 * 8 * 3];
 
+#ifndef MW_WAVES
+#define MW_WAVES 5
+#endif
+
 template <bool NT>
-__global__ __launch_bounds__(192, 5) void window_mfma_kernel(
+__global__ __launch_bounds__(192, MW_WAVES) void window_mfma_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
     const float* __restrict__ base, int64_t n, double* __restrict__ out) {
   using G = Geometry<3>;
@@ -70,6 +74,60 @@ __global__ __launch_bounds__(192, 5) void window_mfma_kernel(
   const int ra = lane & 3, sa = (lane >> 2) & 3, ka = lane >> 4;
   const dwt8_f32x2 rr = {r, r};
   double Q[2][4];
+#ifndef MW_INTERLEAVE
+#define MW_INTERLEAVE 0
+#endif
+#if MW_INTERLEAVE
+  // both groups in one p loop: 24 independent accumulator chains per p step
+  const uint8_t* lbg[2];
+  dwt8_f32x2 bbg[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int el = 4 * g + sa;
+    const bool mine = el < ne;
+    const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
+    bbg[g] = (dwt8_f32x2){b, b};
+    const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
+    lbg[g] = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col + 16 * G::SEGQ * (ra >> 1) +
+             G::FB * (32 * (ra & 1) + ka);
+  }
+  double acc[2][4][3];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float s[4];
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+        s[bi] = (float)*(const int16_t*)(lbg[g] + 16 * G::SEGQ * 2 * bi + G::FB * 4 * p);
+      const dwt8_f32x2 v0 = {s[0], s[1]}, v1 = {s[2], s[3]};
+      const dwt8_f32x2 y0 = v0 * rr - bbg[g], y1 = v1 * rr - bbg[g];
+      const double xa[4] = {(double)y0.x, (double)y0.y, (double)y1.x, (double)y1.y};
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int ji = 0; ji < 3; ++ji)
+          acc[g][bi][ji] = __builtin_amdgcn_mfma_f64_4x4x4f64(
+              xa[bi], Bc[p][ji], p == 0 ? 0.0 : acc[g][bi][ji], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      double q = 0.0;
+      bool first = true;
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int ji = 0; ji < 3; ++ji)
+          if (((bi - ji) & 3) == d) {
+            q = first ? acc[g][bi][ji] : q + acc[g][bi][ji];
+            first = false;
+          }
+      Q[g][d] = q;
+    }
+#else
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int el = 4 * g + sa;
@@ -116,6 +174,7 @@ __global__ __launch_bounds__(192, 5) void window_mfma_kernel(
       Q[g][d] = q;
     }
   }
+#endif
   __syncthreads();  // every wave has read its samples: the window buffer becomes scratch
   // partials: after the 3 KB of feature rows, 512 doubles per wave, slot
   // ((g * 64 + sig * 16 + row * 4 + c) * 4 + class)
