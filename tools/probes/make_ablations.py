@@ -64,6 +64,14 @@ ABLATIONS = {
     const uint32_t v = q[k >> 3][(k >> 1) & 3];
     return (float)(int16_t)((k & 1) ? (v >> 16) : (v & 0xffffu));
   }, r, b, lane & ~7, s, a6, d6);""")]),
+    "noldsread": (
+        "no LDS sample reads: each sample is an opaque per-lane float plus its index (one fp32 "
+        "add in place of the int16 conversion); window DMA, decode and fp64 kept (wrong results)",
+        [("fused.hip",
+          "    dwt8_collapsed_cascade<true>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6,",
+          "    float q = (float)((int)(uintptr_t)own & 1023);  // ablation: no LDS sample reads\n"
+          "    asm volatile(\"\" : \"+v\"(q));\n"
+          "    dwt8_collapsed_cascade<true>([&](int k) { return q + (float)k; }, r, b, gbase, s, a6,")]),
     "nofp64": (
         "fp64 filter bank removed: the 560 FMAs per lane become 64 fp64 adds; DMA, LDS reads and "
         "decode kept (wrong results)",
