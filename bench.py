@@ -94,6 +94,9 @@ def parse():
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather legs")
+    ap.add_argument("--gather-timeout", type=float, default=300.0,
+                    help="seconds the gather legs may take before rank 0 reports the extraction "
+                         "line without them and every rank exits")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: 'gloo' runs the N>1 control flow without RCCL")
     ap.add_argument("--same-device", action="store_true",
@@ -300,17 +303,7 @@ def main():
     norms = torch.linalg.vector_norm(out, dim=1)
     ok_norm = bool(torch.all(torch.isfinite(norms)) and torch.max(torch.abs(norms - 1)) < 1e-12)
 
-    gather = None
-    if distributed and not args.no_gather:
-        try:
-            gather = bench_gather(args, ctx, out, n, C, rank, world, dev, dist)
-        except Exception as exc:  # the extraction line above must still be reported
-            gather = {"op": None, "ms": None, "error": f"{type(exc).__name__}: {exc}"[:300]}
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args, raw, out, ct, C, sp)
-
+    line = None
     if rank == 0:
         workload_key = f"fused_dwt8_c{C}_int16_{n}_{args.numerics}"
         if sp != FRAMES_PER_EPOCH:
@@ -373,10 +366,31 @@ def main():
                                        / 1e12 / FP64_VECTOR_PEAK_TFS, 4)},
                 "ceiling": ceiling_from_profiles(C, args.numerics, n, kernel_ms, kernel_bytes),
             },
-            "cpu_baseline": cpu,
+            "cpu_baseline": None,
         }
-        if alt:
-            line["alt_numerics"] = alt
+
+    if line is not None and alt:
+        line["alt_numerics"] = alt
+
+    # The gathers are the first RCCL traffic between the ranks' own communicators; a hang there
+    # must not cost the extraction line (or keep every rank alive until the launcher's limit).
+    watchdog = _Watchdog()
+    gather = None
+    if distributed and not args.no_gather:
+        watchdog.arm(args.gather_timeout, line,
+                     f"gather legs did not finish within {args.gather_timeout} s")
+        try:
+            gather = bench_gather(args, ctx, out, n, C, rank, world, dev, dist)
+        except Exception as exc:  # the extraction line above must still be reported
+            gather = {"op": None, "ms": None, "error": f"{type(exc).__name__}: {exc}"[:300]}
+        watchdog.disarm()
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(args, raw, out, ct, C, sp)
+
+    if rank == 0:
+        line["cpu_baseline"] = cpu
         if gather:
             line["gather"] = gather
             if gather.get("ms") is not None:
@@ -386,9 +400,41 @@ def main():
                     "unit": "epochs/s", "gather_op": gather["op"]}
         emit(line)
 
+    if distributed:
+        watchdog.arm(60, None, "teardown")  # the line is out; do not hang in teardown
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+    watchdog.disarm()
+
+
+class _Watchdog:
+    """Ends the process if a multi-rank phase hangs: rank 0 first prints the bench line (when it
+    has not been printed yet) with the phase's error, so the extraction measurement survives."""
+
+    def __init__(self):
+        self._timer = None
+
+    def arm(self, seconds, line, what):
+        import threading
+
+        def fire():
+            if line is not None:
+                line["gather"] = {"op": None, "ms": None, "error": what}
+                emit(line)
+            sys.stderr.write(f"bench.py: {what}; exiting\n")
+            sys.stderr.flush()
+            os._exit(0)  # the phase is outside the measurement; its error is in the line
+
+        self.disarm()
+        self._timer = threading.Timer(seconds, fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def disarm(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
 
 
 def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):

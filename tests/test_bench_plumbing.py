@@ -53,3 +53,25 @@ def test_whole_path_ceiling_adds_the_baseline_pass():
     assert 0.5 < c["frac"] < 0.8
     assert bench.whole_path_ceiling(32, "fma", 1, 1.0, 1) is None
     assert bench.whole_path_ceiling(3, "exact", 1, 1.0, 1) is None
+
+
+def test_watchdog_reports_the_line_and_exits_when_a_phase_hangs():
+    """A multi-rank phase that never returns (a gather stuck in RCCL) must not cost the extraction
+    line: rank 0 prints it with the phase's error and the process exits 0."""
+    import subprocess
+    import sys
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "w = bench._Watchdog(); w.arm(0.5, {'metric': 'm', 'value': 1.0}, 'gather hung')\n"
+            "time.sleep(30)\n") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=20)
+    assert r.returncode == 0
+    line = json.loads(r.stdout.strip())
+    assert line["value"] == 1.0 and line["gather"]["error"] == "gather hung"
+
+
+def test_watchdog_disarmed_phase_does_not_fire():
+    import time
+    w = bench._Watchdog()
+    w.arm(0.2, None, "teardown")
+    w.disarm()
+    time.sleep(0.4)  # still alive: the timer was cancelled
