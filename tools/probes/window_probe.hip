@@ -4,6 +4,7 @@
 //
 //   hipcc ... -DFUSED_SRC='"build/v1/fused.hip"' window_probe.hip -o window_probe_v1
 //   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
+//   PROBE_BASELINE=1: time the baseline kernel alone; PROBE_STEP=1: baseline + window per launch
 //
 // Phase timestamps (per-workgroup s_memrealtime at each phase boundary):
 //   restore_variant.sh phase_timestamps_fused, then -DFUSED_SRC='"<dir>/fused.hip"' -DPROBE_TIMESTAMPS
@@ -64,9 +65,15 @@ int main() {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const bool time_baseline = getenv("PROBE_BASELINE") != nullptr;
-  for (int r = 0; r < 200; ++r) time_baseline ? baseline() : window();
+  const bool time_step = getenv("PROBE_STEP") != nullptr;  // baseline + window, as bench.py's step
+  auto one = [&] {
+    if (time_step) { baseline(); window(); }
+    else if (time_baseline) baseline();
+    else window();
+  };
+  for (int r = 0; r < 200; ++r) one();
   (void)hipEventRecord(a);
-  for (int r = 0; r < iters; ++r) time_baseline ? baseline() : window();
+  for (int r = 0; r < iters; ++r) one();
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms;
@@ -122,6 +129,6 @@ int main() {
   const hipError_t e = hipGetLastError();
   printf("%s %s %s: %.4f ms per launch (%d launches)  checksum %.17g %.17g  %s\n",
          wide ? "wide c32" : "window c3", fast ? "fma" : "exact",
-         time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
+         time_step ? "step" : time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
   return e == hipSuccess ? 0 : 1;
 }
