@@ -21,12 +21,15 @@ DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane,
   dma_drain();"""
 
 FMA_BODY = """#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      if (n + 32 * j >= 280) continue;
-      const double t = j < kH5Cols ? T[j] : tab[kH5Tail + n];
-      P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
-      if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
-      else P[j] = __builtin_fma(x1, t, P[j]);
+    for (int i = 0; i < 4; ++i) {
+      U[i] = n == 0 ? x1 * T[2 * i] : __builtin_fma(x1, T[2 * i], U[i]);
+      V[i] = n == 0 ? x0 * T[2 * i + 1] : __builtin_fma(x0, T[2 * i + 1], V[i]);
+      W[i] = n == 0 ? xs * S[i] : __builtin_fma(xs, S[i], W[i]);
+    }
+    if (n < 24) {  // tap j = 8 (H5[256 + n]), direct
+      const double t = tn[kH5Tail + n];
+      P[8] = n == 0 ? x1 * t : __builtin_fma(x1, t, P[8]);
+      P[9] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[9]);
     }"""
 
 ABLATIONS = {
@@ -34,6 +37,10 @@ ABLATIONS = {
         "fma filter bank as the round-2 level-by-level cascade with partial-sum halos "
         "(A/B against the collapsed filter)",
         [("dwt8.h", "#define EEGFX_COLLAPSED 1", "#define EEGFX_COLLAPSED 0")]),
+    "direct": (
+        "each pair's update in the direct form (18 multiply-adds) instead of the two-term "
+        "Karatsuba form (14 + one add): A/B of the change",
+        [("dwt8.h", "#define EEGFX_KARATSUBA 1", "#define EEGFX_KARATSUBA 0")]),
     "nodma": (
         "no window DMA: removes the HBM window reads and the LDS writes; LDS reads, decode and "
         "fp64 kept (wrong results)",
@@ -73,10 +80,13 @@ ABLATIONS = {
           "    asm volatile(\"\" : \"+v\"(q));\n"
           "    dwt8_collapsed_cascade<true>([&](int k) { return q + (float)k; }, r, b, gbase, s, a6,")]),
     "nofp64": (
-        "fp64 filter bank removed: the 560 FMAs per lane become 64 fp64 adds; DMA, LDS reads and "
-        "decode kept (wrong results)",
-        [("dwt8.h", FMA_BODY, """    (void)T;  // ablation: no fp64 filter work, the decoded samples are summed
-    if (n < 10) { P[n] = x0 + x1; } else { P[n % 10] += x0; P[(n + 5) % 10] += x1; }""")]),
+        "fp64 filter bank removed: the 464 multiply-adds per lane become 64 fp64 adds; DMA, LDS "
+        "reads and decode kept (wrong results)",
+        [("dwt8.h", FMA_BODY, """    (void)T; (void)S;  // ablation: no fp64 filter work, the decoded samples are summed
+    if (n == 0) {
+      for (int i = 0; i < 4; ++i) { U[i] = x1; V[i] = x0; W[i] = xs; }
+      P[8] = x1; P[9] = x0;
+    } else { U[n & 3] += x1; V[n & 3] += x0; }""")]),
 }
 
 
