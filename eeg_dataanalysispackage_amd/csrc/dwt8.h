@@ -382,17 +382,17 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // even and odd taps, U += Te x1, V += To x0, W += (Te + To)(x0 + x1) over all pairs, and
 // P[2i] = U[i] + V[i-1], P[2i+1] = W[i] - U[i] - V[i] once at the end.  That is 12 instead of 16
 // multiply-adds per pair for taps j < 8 (+ one exact add, x0 + x1), the tap j = 8 direct:
-// 464 instead of 560 per lane.  The pair-sum taps come exactly rounded from dwt8_taps.h.
+// 464 instead of 560 per lane (VALU per wave 1,083 -> 999 in the c3 kernel, 1,050 -> 958 in c32).
+// The pair-sum taps come exactly rounded from dwt8_taps.h.
 static __constant__ double kH5[kH5Size] = EEGFX_H5_TABLE;
 #ifndef EEGFX_KARATSUBA
 #define EEGFX_KARATSUBA 1
 #endif
 
-// REGION: one scheduling region per sample pair.  In the c3 window kernel the compiler otherwise
-// hoists tap rows into SGPRs and spills them to VGPR lanes (870 -> 854 VALU per wave, -0.7 %); the
-// c32 kernel does not spill without it, and measured +0.4 % with it (more exposed scalar-load
-// latency), so it leaves it off.
-template <bool REGION = false, typename Fetch>
+// EEGFX_KARATSUBA 0 (A/B builds only, tools/probes/ablations/direct.patch) keeps the direct form
+// of round 3's first version, with one scheduling region per pair (without it the c3 kernel
+// hoisted tap rows into SGPRs and spilled them to VGPR lanes).
+template <typename Fetch>
 __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
                                                        int s, double& a6, double& d6) {
   typedef const __attribute__((address_space(4))) double* const_f64_ptr;
@@ -402,18 +402,20 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   double P[10];  // P[j + 1]
 #if EEGFX_KARATSUBA
   double U[4], V[4], W[4];
+  // the samples are fetched two pairs ahead of their use (the per-pair ordering below otherwise
+  // leaves each pair's sample reads exposed: -2.0 % c3, -2.6 % c32)
+  dwt8_f32x2 vq[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) vq[d] = dwt8_f32x2{fetch(d), fetch(d + 32)};
 #pragma unroll
   for (int n = 0; n < 32; ++n) {
-    const dwt8_f32x2 v = {fetch(n), fetch(n + 32)};
+    const dwt8_f32x2 v = vq[n % 2];
+    if (n + 2 < 32) vq[n % 2] = dwt8_f32x2{fetch(n + 2), fetch(n + 2 + 32)};
     const dwt8_f32x2 y = v * rr - bb;
     const double x0 = (double)y.x, x1 = (double)y.y;
     const double xs = x0 + x1;  // exact: two floats
-    // a fresh opaque copy of the table base per pair: the pair's 13 taps are loaded in its own
-    // scheduling region, not ahead of it
-    const_f64_ptr tn = tab;
-    asm volatile("" : "+s"(tn));
-    const const_f64_ptr T = tn + n * kH5Cols;
-    const const_f64_ptr S = tn + kH5Sum + n * kH5Sums;
+    const const_f64_ptr T = tab + n * kH5Cols;
+    const const_f64_ptr S = tab + kH5Sum + n * kH5Sums;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       U[i] = n == 0 ? x1 * T[2 * i] : __builtin_fma(x1, T[2 * i], U[i]);
@@ -421,7 +423,7 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
       W[i] = n == 0 ? xs * S[i] : __builtin_fma(xs, S[i], W[i]);
     }
     if (n < 24) {  // tap j = 8 (H5[256 + n]), direct
-      const double t = tn[kH5Tail + n];
+      const double t = tab[kH5Tail + n];
       P[8] = n == 0 ? x1 * t : __builtin_fma(x1, t, P[8]);
       P[9] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[9]);
     }
@@ -430,7 +432,6 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
     asm volatile("" : "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(U[3]), "+v"(V[0]), "+v"(V[1]),
                  "+v"(V[2]), "+v"(V[3]), "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]),
                  "+v"(P[8]), "+v"(P[9]));
-    if constexpr (REGION) __builtin_amdgcn_sched_barrier(0);
   }
   P[0] = U[0];
 #pragma unroll
@@ -454,7 +455,7 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
       if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
       else P[j] = __builtin_fma(x1, t, P[j]);
     }
-    if constexpr (REGION) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 #endif
   double a5[2 + 8];

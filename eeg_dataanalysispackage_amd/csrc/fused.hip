@@ -209,8 +209,7 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
                                             float b, int gbase, int s, double& a6, double& d6) {
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
-    dwt8_collapsed_cascade<true>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6,
-                                 d6);
+    dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
 #else
     dwt8_fast_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
 #endif

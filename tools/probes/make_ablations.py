@@ -27,7 +27,7 @@ FMA_BODY = """#pragma unroll
       W[i] = n == 0 ? xs * S[i] : __builtin_fma(xs, S[i], W[i]);
     }
     if (n < 24) {  // tap j = 8 (H5[256 + n]), direct
-      const double t = tn[kH5Tail + n];
+      const double t = tab[kH5Tail + n];
       P[8] = n == 0 ? x1 * t : __builtin_fma(x1, t, P[8]);
       P[9] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[9]);
     }"""
@@ -67,7 +67,7 @@ ABLATIONS = {
 #pragma unroll
     for (int i = 0; i < 8; ++i) q[i] = src[i];
   }
-  dwt8_collapsed_cascade<true>([&](int k) {
+  dwt8_collapsed_cascade([&](int k) {
     const uint32_t v = q[k >> 3][(k >> 1) & 3];
     return (float)(int16_t)((k & 1) ? (v >> 16) : (v & 0xffffu));
   }, r, b, lane & ~7, s, a6, d6);""")]),
@@ -75,10 +75,10 @@ ABLATIONS = {
         "no LDS sample reads: each sample is an opaque per-lane float plus its index (one fp32 "
         "add in place of the int16 conversion); window DMA, decode and fp64 kept (wrong results)",
         [("fused.hip",
-          "    dwt8_collapsed_cascade<true>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6,",
+          "    dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);",
           "    float q = (float)((int)(uintptr_t)own & 1023);  // ablation: no LDS sample reads\n"
           "    asm volatile(\"\" : \"+v\"(q));\n"
-          "    dwt8_collapsed_cascade<true>([&](int k) { return q + (float)k; }, r, b, gbase, s, a6,")]),
+          "    dwt8_collapsed_cascade([&](int k) { return q + (float)k; }, r, b, gbase, s, a6, d6);")]),
     "nofp64": (
         "fp64 filter bank removed: the 464 multiply-adds per lane become 64 fp64 adds; DMA, LDS "
         "reads and decode kept (wrong results)",
