@@ -21,6 +21,7 @@ Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").  Extra legs:
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -107,13 +108,23 @@ def parse():
     return ap.parse_args()
 
 
+def run_tag_order(name):
+    """Order of the run tags that prefix profiles/ files: r<round><letters>, the letters counted
+    like spreadsheet columns (r03z < r03aa < r03ab), so the newest run sorts last."""
+    m = re.match(r"r(\d+)([a-z]*)", name)
+    if not m:
+        return (-1, 0, name)
+    return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+
 def traffic_from_profiles(workload_key):
-    """HBM bytes per launch from the committed PMC summary (profiles/*traffic*.json)."""
+    """HBM bytes per launch from the committed PMC summary (profiles/*traffic*.json): the newest
+    run's file for the workload."""
     best = None
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
         return None
-    for f in sorted(os.listdir(pdir)):
+    for f in sorted(os.listdir(pdir), key=run_tag_order):
         if f.endswith(".json") and "traffic" in f:
             try:
                 d = json.load(open(os.path.join(pdir, f)))

@@ -24,12 +24,20 @@ def test_traffic_reader_takes_the_newest_summary():
     got = bench.traffic_from_profiles(key)
     assert got is not None and got["workload_key"] == key
     pdir = os.path.join(REPO, "profiles")
-    names = sorted(f for f in os.listdir(pdir) if f.endswith(".json") and "traffic" in f and
-                   json.load(open(os.path.join(pdir, f))).get("workload_key") == key)
+    names = sorted((f for f in os.listdir(pdir) if f.endswith(".json") and "traffic" in f and
+                    json.load(open(os.path.join(pdir, f))).get("workload_key") == key),
+                   key=bench.run_tag_order)
+    assert names[-1].startswith("r03ab_")  # the newest run of round 3
     assert got == json.load(open(os.path.join(pdir, names[-1])))
     # FETCH_SIZE x2 (gfx950) + WRITE_SIZE over the algorithmic 3,476 B per epoch: a few % over
     assert 1.0 <= got["hbm_bytes_per_launch"] / 3.476e9 < 1.1
     assert bench.traffic_from_profiles("no such workload") is None
+
+
+def test_run_tags_order_like_spreadsheet_columns():
+    tags = ["r03ab_x", "r02n_x", "r03k_x", "r03aa_x", "r03z_x", "r03h_x", "r01b_x"]
+    assert sorted(tags, key=bench.run_tag_order) == [
+        "r01b_x", "r02n_x", "r03h_x", "r03k_x", "r03z_x", "r03aa_x", "r03ab_x"]
 
 
 def test_ceiling_reader_scales_to_the_launch():
