@@ -388,6 +388,17 @@ static __constant__ double kH5[kH5Size] = EEGFX_H5_TABLE;
 #ifndef EEGFX_KARATSUBA
 #define EEGFX_KARATSUBA 1
 #endif
+// The four-point (Toom) form goes one step further (EEGFX_TOOM, the default): the nine taps of
+// row n in three blocks by j mod 3, B0, B1, B2, and the pair's product (B0 + w B1 + w^2 B2)
+// (x1 + w x0) evaluated at w = 0, infinity, 1 and -1.  The lane accumulates A0 += B0 x1,
+// Ai += B2 x0, Bp += (B0 + B1 + B2)/2 (x1 + x0) and Bm += (B0 - B1 + B2)/2 (x1 - x0), three
+// entries each, and interpolates once: with c0 = A0, c3 = Ai, c1 = Bp - Bm - c3, c2 = Bp + Bm - c0,
+// P[3q + r] collects c_r[q] (+ c3[q - 1] for r = 0).  12 multiply-adds and two exact adds per pair
+// (11 + 2 once tap 280 is passed): 440 per lane instead of 464; the halving is exact and folded
+// into the exactly rounded constants of dwt8_taps.h.  One 96-byte constant row per pair.
+#ifndef EEGFX_TOOM
+#define EEGFX_TOOM 1
+#endif
 
 // EEGFX_KARATSUBA 0 (A/B builds only, tools/probes/ablations/direct.patch) keeps the direct form
 // of round 3's first version, with one scheduling region per pair (without it the c3 kernel
@@ -401,7 +412,11 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   const dwt8_f32x2 rr = {r, r}, bb = {b, b};
   double P[10];  // P[j + 1]
 #if EEGFX_KARATSUBA
+#if EEGFX_TOOM
+  double A0[3], Ai[3], Bp[3], Bm[3];
+#else
   double U[4], V[4], W[4];
+#endif
   // the samples are fetched two pairs ahead of their use (the per-pair ordering below otherwise
   // leaves each pair's sample reads exposed: -2.0 % c3, -2.6 % c32)
   dwt8_f32x2 vq[2];
@@ -413,6 +428,27 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
     if (n + 2 < 32) vq[n % 2] = dwt8_f32x2{fetch(n + 2), fetch(n + 2 + 32)};
     const dwt8_f32x2 y = v * rr - bb;
     const double x0 = (double)y.x, x1 = (double)y.y;
+#if EEGFX_TOOM
+    const double xp = x1 + x0, xm = x1 - x0;  // exact: two floats
+    const const_f64_ptr R = tab + kH5Toom + n * kH5ToomCols;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
+      if (n + 32 * (3 * q + 2) < 280) Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
+      Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
+      Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
+    }
+    asm volatile("" : "+v"(A0[0]), "+v"(A0[1]), "+v"(A0[2]), "+v"(Ai[0]), "+v"(Ai[1]), "+v"(Ai[2]),
+                 "+v"(Bp[0]), "+v"(Bp[1]), "+v"(Bp[2]), "+v"(Bm[0]), "+v"(Bm[1]), "+v"(Bm[2]));
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    P[3 * q] = q > 0 ? A0[q] + Ai[q - 1] : A0[q];
+    P[3 * q + 1] = Bp[q] - Bm[q] - Ai[q];
+    P[3 * q + 2] = Bp[q] + Bm[q] - A0[q];
+  }
+  P[9] = Ai[2];
+#else
     const double xs = x0 + x1;  // exact: two floats
     const const_f64_ptr T = tab + n * kH5Cols;
     const const_f64_ptr S = tab + kH5Sum + n * kH5Sums;
@@ -440,6 +476,7 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
     if (i < 3) P[2 * i + 2] = U[i + 1] + V[i];
   }
   P[8] += V[3];
+#endif
 #else
 #pragma unroll
   for (int n = 0; n < 32; ++n) {

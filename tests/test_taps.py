@@ -88,8 +88,49 @@ def test_lane_algebra_matches_the_cascade():
         for _lev in range(5):
             N = len(a)
             a = np.array([sum(h[t] * a[(2 * k + t) % N] for t in range(10)) for k in range(N // 2)])
-        for got in (_lane_model(x, tab), _lane_model(x, tab, gen_taps.tap_sum)):
+        for got in (_lane_model(x, tab), _lane_model(x, tab, gen_taps.tap_sum),
+                    _toom_lane_model(x, gen_taps.toom_rows())):
             assert np.max(np.abs(got - a)) <= 1e-12 * np.max(np.abs(a))
+
+
+def _toom_lane_model(x, rows):
+    """The four-point (Toom) form of each pair's update: the nine taps of row n in three blocks
+    (j mod 3); A0 += B0 x1, Ai += B2 x0, Bp += (B0+B1+B2)/2 (x1+x0), Bm += (B0-B1+B2)/2 (x1-x0)."""
+    P = np.zeros((8, 10))
+    for s in range(8):
+        xs = x[64 * s:64 * s + 64]
+        A0, Ai, Bp, Bm = np.zeros(3), np.zeros(3), np.zeros(3), np.zeros(3)
+        for n in range(32):
+            x0, x1 = xs[n], xs[n + 32]
+            R = rows[n]
+            for q in range(3):
+                A0[q] += x1 * R[q]
+                Ai[q] += x0 * R[3 + q]
+                Bp[q] += (x1 + x0) * R[6 + q]
+                Bm[q] += (x1 - x0) * R[9 + q]
+        for q in range(3):
+            P[s][3 * q] = A0[q] + (Ai[q - 1] if q else 0.0)
+            P[s][3 * q + 1] = Bp[q] - Bm[q] - Ai[q]
+            P[s][3 * q + 2] = Bp[q] + Bm[q] - A0[q]
+        P[s][9] = Ai[2]
+    a5 = np.zeros(16)
+    for s in range(8):
+        a5[2 * s] = P[s][1] + sum(P[(s + d) % 8][2 * d + 1] for d in range(1, 5))
+        a5[2 * s + 1] = P[s][0] + sum(P[(s + d) % 8][2 * d] for d in range(1, 5))
+    return a5
+
+
+def test_toom_rows_are_exactly_rounded():
+    """B0, B2 and the halved block sums (B0 + B1 + B2) / 2, (B0 - B1 + B2) / 2, exact and rounded
+    once (0 past tap 279)."""
+    H = gen_taps.combined_taps()
+    h = lambda m: H[m] if m < 280 else 0
+    for n in range(32):
+        R = gen_taps.toom_rows()[n]
+        for q in range(3):
+            b0, b1, b2 = (h(n + 32 * (3 * q + r)) for r in range(3))
+            assert R[q] == float(b0) and R[3 + q] == float(b2)
+            assert R[6 + q] == float((b0 + b1 + b2) / 2) and R[9 + q] == float((b0 - b1 + b2) / 2)
 
 
 def test_pair_sums_are_exactly_rounded():
