@@ -378,31 +378,23 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // differs from the reference's, inside the 1e-9 contract; EXACT keeps the level-by-level cascade.
 //
 // Each pair's update is a product of polynomials, P(z) += T_n(z) (x1 + z x0) with
-// T_n(z) = sum_j H5[n + 32 j] z^j, and runs in the two-term (Karatsuba) form: with T_n split into
-// even and odd taps, U += Te x1, V += To x0, W += (Te + To)(x0 + x1) over all pairs, and
-// P[2i] = U[i] + V[i-1], P[2i+1] = W[i] - U[i] - V[i] once at the end.  That is 12 instead of 16
-// multiply-adds per pair for taps j < 8 (+ one exact add, x0 + x1), the tap j = 8 direct:
-// 464 instead of 560 per lane (VALU per wave 1,083 -> 999 in the c3 kernel, 1,050 -> 958 in c32).
-// The pair-sum taps come exactly rounded from dwt8_taps.h.
+// T_n(z) = sum_j H5[n + 32 j] z^j, and runs in a four-point (Toom) form: the nine taps in three
+// blocks by j mod 3, T_n(z) = B0(z^3) + z B1(z^3) + z^2 B2(z^3), and the product
+// (B0 + w B1 + w^2 B2)(x1 + w x0) = c0 + w c1 + w^2 c2 + w^3 c3 evaluated at w = 0, infinity, 1 and
+// -1.  Over all pairs the lane accumulates A0 += B0 x1, Ai += B2 x0, Bp += (B0 + B1 + B2)/2 (x1 + x0)
+// and Bm += (B0 - B1 + B2)/2 (x1 - x0), three entries each, and interpolates once:
+// c0 = A0, c3 = Ai, c1 = Bp - Bm - c3, c2 = Bp + Bm - c0, P[3q + r] = c_r[q] (+ c3[q - 1] for r = 0).
+// That is 12 multiply-adds and two exact adds (x1 +- x0, two floats) per pair, 11 + 2 once tap 280
+// is passed: 440 per lane instead of the direct form's 560.  The constants are exact rational sums
+// halved and rounded once (dwt8_taps.h), one 96-byte row per pair.
+//   Measured: the two-term Karatsuba form (464 per lane, `git show
+//   682923c:eeg_dataanalysispackage_amd/csrc/dwt8.h`, -DEEGFX_TOOM=0) was 2.2 % slower; the direct
+//   form (EEGFX_TOOM 0 here, tools/probes/ablations/direct.patch) 4-6 % slower still.
 static __constant__ double kH5[kH5Size] = EEGFX_H5_TABLE;
-#ifndef EEGFX_KARATSUBA
-#define EEGFX_KARATSUBA 1
-#endif
-// The four-point (Toom) form goes one step further (EEGFX_TOOM, the default): the nine taps of
-// row n in three blocks by j mod 3, B0, B1, B2, and the pair's product (B0 + w B1 + w^2 B2)
-// (x1 + w x0) evaluated at w = 0, infinity, 1 and -1.  The lane accumulates A0 += B0 x1,
-// Ai += B2 x0, Bp += (B0 + B1 + B2)/2 (x1 + x0) and Bm += (B0 - B1 + B2)/2 (x1 - x0), three
-// entries each, and interpolates once: with c0 = A0, c3 = Ai, c1 = Bp - Bm - c3, c2 = Bp + Bm - c0,
-// P[3q + r] collects c_r[q] (+ c3[q - 1] for r = 0).  12 multiply-adds and two exact adds per pair
-// (11 + 2 once tap 280 is passed): 440 per lane instead of 464; the halving is exact and folded
-// into the exactly rounded constants of dwt8_taps.h.  One 96-byte constant row per pair.
 #ifndef EEGFX_TOOM
 #define EEGFX_TOOM 1
 #endif
 
-// EEGFX_KARATSUBA 0 (A/B builds only, tools/probes/ablations/direct.patch) keeps the direct form
-// of round 3's first version, with one scheduling region per pair (without it the c3 kernel
-// hoisted tap rows into SGPRs and spilled them to VGPR lanes).
 template <typename Fetch>
 __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
                                                        int s, double& a6, double& d6) {
@@ -411,33 +403,32 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   asm volatile("" : "+s"(tab));  // scalar loads of the table, not per-tap literal moves
   const dwt8_f32x2 rr = {r, r}, bb = {b, b};
   double P[10];  // P[j + 1]
-#if EEGFX_KARATSUBA
 #if EEGFX_TOOM
   double A0[3], Ai[3], Bp[3], Bm[3];
-#else
-  double U[4], V[4], W[4];
-#endif
   // the samples are fetched two pairs ahead of their use (the per-pair ordering below otherwise
-  // leaves each pair's sample reads exposed: -2.0 % c3, -2.6 % c32)
-  dwt8_f32x2 vq[2];
+  // leaves each pair's sample reads exposed)
+  typedef decltype(+fetch(0)) Raw;  // int for int16 samples (converted at use), float for float
+  Raw vq[2][2];
 #pragma unroll
-  for (int d = 0; d < 2; ++d) vq[d] = dwt8_f32x2{fetch(d), fetch(d + 32)};
+  for (int d = 0; d < 2; ++d) { vq[d][0] = fetch(d); vq[d][1] = fetch(d + 32); }
 #pragma unroll
   for (int n = 0; n < 32; ++n) {
-    const dwt8_f32x2 v = vq[n % 2];
-    if (n + 2 < 32) vq[n % 2] = dwt8_f32x2{fetch(n + 2), fetch(n + 2 + 32)};
+    const dwt8_f32x2 v = {(float)vq[n % 2][0], (float)vq[n % 2][1]};
+    if (n + 2 < 32) { vq[n % 2][0] = fetch(n + 2); vq[n % 2][1] = fetch(n + 2 + 32); }
     const dwt8_f32x2 y = v * rr - bb;
     const double x0 = (double)y.x, x1 = (double)y.y;
-#if EEGFX_TOOM
     const double xp = x1 + x0, xm = x1 - x0;  // exact: two floats
-    const const_f64_ptr R = tab + kH5Toom + n * kH5ToomCols;
+    const const_f64_ptr R = tab + n * kH5Cols;  // this pair's 12 constants (96 bytes)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
-      if (n + 32 * (3 * q + 2) < 280) Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
+      if (n + 32 * (3 * q + 2) < 280)
+        Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
       Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
       Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
     }
+    // The pair's updates complete here: without this, the IR ends up ordered chain by chain (all
+    // 64 sample reads and 32 constant rows first, every multiply-add after them), which spills.
     asm volatile("" : "+v"(A0[0]), "+v"(A0[1]), "+v"(A0[2]), "+v"(Ai[0]), "+v"(Ai[1]), "+v"(Ai[2]),
                  "+v"(Bp[0]), "+v"(Bp[1]), "+v"(Bp[2]), "+v"(Bm[0]), "+v"(Bm[1]), "+v"(Bm[2]));
   }
@@ -449,45 +440,17 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   }
   P[9] = Ai[2];
 #else
-    const double xs = x0 + x1;  // exact: two floats
-    const const_f64_ptr T = tab + n * kH5Cols;
-    const const_f64_ptr S = tab + kH5Sum + n * kH5Sums;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      U[i] = n == 0 ? x1 * T[2 * i] : __builtin_fma(x1, T[2 * i], U[i]);
-      V[i] = n == 0 ? x0 * T[2 * i + 1] : __builtin_fma(x0, T[2 * i + 1], V[i]);
-      W[i] = n == 0 ? xs * S[i] : __builtin_fma(xs, S[i], W[i]);
-    }
-    if (n < 24) {  // tap j = 8 (H5[256 + n]), direct
-      const double t = tab[kH5Tail + n];
-      P[8] = n == 0 ? x1 * t : __builtin_fma(x1, t, P[8]);
-      P[9] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[9]);
-    }
-    // The pair's updates complete here: without this, the IR ends up ordered chain by chain (all
-    // 64 sample reads and 32 tap rows first, every multiply-add after them), which spills.
-    asm volatile("" : "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(U[3]), "+v"(V[0]), "+v"(V[1]),
-                 "+v"(V[2]), "+v"(V[3]), "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]),
-                 "+v"(P[8]), "+v"(P[9]));
-  }
-  P[0] = U[0];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    P[2 * i + 1] = W[i] - U[i] - V[i];
-    if (i < 3) P[2 * i + 2] = U[i + 1] + V[i];
-  }
-  P[8] += V[3];
-#endif
-#else
+  // the direct form (A/B builds only): 18 multiply-adds per pair, one scheduling region per pair
+  // (without it the c3 kernel hoisted tap rows into SGPRs and spilled them to VGPR lanes)
 #pragma unroll
   for (int n = 0; n < 32; ++n) {
-    const dwt8_f32x2 v = {fetch(n), fetch(n + 32)};
+    const dwt8_f32x2 v = {(float)fetch(n), (float)fetch(n + 32)};
     const dwt8_f32x2 y = v * rr - bb;
     const double x0 = (double)y.x, x1 = (double)y.y;
-    const const_f64_ptr T = tab + n * kH5Cols;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       if (n + 32 * j >= 280) continue;
-      const double t = j < kH5Cols ? T[j] : tab[kH5Tail + n];
+      const double t = j < kH5DirectCols ? tab[kH5Direct + n * kH5DirectCols + j] : tab[kH5Tail + n];
       P[j + 1] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[j + 1]);   // sample n -> accumulator j
       if (n == 0 && j == 0) P[0] = x1 * t;                            // sample n + 32 -> j - 1
       else P[j] = __builtin_fma(x1, t, P[j]);

@@ -4,7 +4,7 @@ dwt8_collapsed_cascade (csrc/dwt8.h) runs levels 1-5 of the fe=dwt-8 pyramid
 (WaveletTransform.java:126-137) as one 280-tap filter at stride 32.  These
 checks pin the committed header to gen_taps.py, the table to the exact rational composition of
 the 12-decimal taps, and the kernel's lane algebra (ten partial sums per lane, four received from
-lanes s+1..s+4; each pair's update in the direct and in the two-term Karatsuba form) to the
+lanes s+1..s+4; each pair's update in the direct and in the four-point Toom form) to the
 level-by-level cascade of the oracle.
 """
 import ctypes
@@ -40,37 +40,17 @@ def test_table_is_the_rounded_exact_composition():
     assert tail[24:] == (0.0,) * 8
 
 
-def _lane_model(x, tab, tab_sum=None):
-    """The kernel's arithmetic order for one 512-sample signal (8 lanes), in numpy doubles: the
-    direct pair update, or (tab_sum given) the two-term Karatsuba form of dwt8_collapsed_cascade."""
+def _lane_model(x, tab):
+    """The direct form's arithmetic order for one 512-sample signal (8 lanes), in numpy doubles."""
     P = np.zeros((8, 10))
     for s in range(8):
         xs = x[64 * s:64 * s + 64]
-        if tab_sum is None:
-            for n in range(32):
-                for j in range(9):
-                    if n + 32 * j >= 280:
-                        continue
-                    P[s][j + 1] = P[s][j + 1] + xs[n] * tab(n, j)
-                    P[s][j] = P[s][j] + xs[n + 32] * tab(n, j)
-            continue
-        U, V, W = np.zeros(4), np.zeros(4), np.zeros(4)
         for n in range(32):
-            x0, x1 = xs[n], xs[n + 32]
-            xsum = x0 + x1
-            for i in range(4):
-                U[i] += x1 * tab(n, 2 * i)
-                V[i] += x0 * tab(n, 2 * i + 1)
-                W[i] += xsum * tab_sum(n, i)
-            if n < 24:
-                P[s][8] += x1 * tab(n, 8)
-                P[s][9] += x0 * tab(n, 8)
-        P[s][0] = U[0]
-        for i in range(4):
-            P[s][2 * i + 1] = W[i] - U[i] - V[i]
-            if i < 3:
-                P[s][2 * i + 2] = U[i + 1] + V[i]
-        P[s][8] += V[3]
+            for j in range(9):
+                if n + 32 * j >= 280:
+                    continue
+                P[s][j + 1] = P[s][j + 1] + xs[n] * tab(n, j)
+                P[s][j] = P[s][j] + xs[n + 32] * tab(n, j)
     a5 = np.zeros(16)
     for s in range(8):
         a5[2 * s] = P[s][1] + sum(P[(s + d) % 8][2 * d + 1] for d in range(1, 5))
@@ -88,8 +68,7 @@ def test_lane_algebra_matches_the_cascade():
         for _lev in range(5):
             N = len(a)
             a = np.array([sum(h[t] * a[(2 * k + t) % N] for t in range(10)) for k in range(N // 2)])
-        for got in (_lane_model(x, tab), _lane_model(x, tab, gen_taps.tap_sum),
-                    _toom_lane_model(x, gen_taps.toom_rows())):
+        for got in (_lane_model(x, tab), _toom_lane_model(x, gen_taps.toom_rows())):
             assert np.max(np.abs(got - a)) <= 1e-12 * np.max(np.abs(a))
 
 
@@ -131,15 +110,6 @@ def test_toom_rows_are_exactly_rounded():
             b0, b1, b2 = (h(n + 32 * (3 * q + r)) for r in range(3))
             assert R[q] == float(b0) and R[3 + q] == float(b2)
             assert R[6 + q] == float((b0 + b1 + b2) / 2) and R[9 + q] == float((b0 - b1 + b2) / 2)
-
-
-def test_pair_sums_are_exactly_rounded():
-    """The Karatsuba taps H5[n + 64 i] + H5[n + 64 i + 32], summed exactly and rounded once."""
-    H = gen_taps.combined_taps()
-    for n in range(32):
-        for i in range(4):
-            assert gen_taps.tap_sum(n, i) == float(H[n + 64 * i] + H[n + 64 * i + 32])
-            assert n + 64 * i + 32 < 280
 
 
 def test_literals_are_the_kernel_taps():

@@ -21,15 +21,12 @@ DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane,
   dma_drain();"""
 
 FMA_BODY = """#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      U[i] = n == 0 ? x1 * T[2 * i] : __builtin_fma(x1, T[2 * i], U[i]);
-      V[i] = n == 0 ? x0 * T[2 * i + 1] : __builtin_fma(x0, T[2 * i + 1], V[i]);
-      W[i] = n == 0 ? xs * S[i] : __builtin_fma(xs, S[i], W[i]);
-    }
-    if (n < 24) {  // tap j = 8 (H5[256 + n]), direct
-      const double t = tab[kH5Tail + n];
-      P[8] = n == 0 ? x1 * t : __builtin_fma(x1, t, P[8]);
-      P[9] = n == 0 ? x0 * t : __builtin_fma(x0, t, P[9]);
+    for (int q = 0; q < 3; ++q) {
+      A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
+      if (n + 32 * (3 * q + 2) < 280)
+        Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
+      Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
+      Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
     }"""
 
 ABLATIONS = {
@@ -38,9 +35,9 @@ ABLATIONS = {
         "(A/B against the collapsed filter)",
         [("dwt8.h", "#define EEGFX_COLLAPSED 1", "#define EEGFX_COLLAPSED 0")]),
     "direct": (
-        "each pair's update in the direct form (18 multiply-adds) instead of the two-term "
-        "Karatsuba form (14 + one add): A/B of the change",
-        [("dwt8.h", "#define EEGFX_KARATSUBA 1", "#define EEGFX_KARATSUBA 0")]),
+        "each pair's update in the direct form (18 multiply-adds) instead of the four-point Toom "
+        "form (12 + two adds): A/B of the change",
+        [("dwt8.h", "#define EEGFX_TOOM 1", "#define EEGFX_TOOM 0")]),
     "nodma": (
         "no window DMA: removes the HBM window reads and the LDS writes; LDS reads, decode and "
         "fp64 kept (wrong results)",
@@ -80,13 +77,12 @@ ABLATIONS = {
           "    asm volatile(\"\" : \"+v\"(q));\n"
           "    dwt8_collapsed_cascade([&](int k) { return q + (float)k; }, r, b, gbase, s, a6, d6);")]),
     "nofp64": (
-        "fp64 filter bank removed: the 464 multiply-adds per lane become 64 fp64 adds; DMA, LDS "
-        "reads and decode kept (wrong results)",
-        [("dwt8.h", FMA_BODY, """    (void)T; (void)S;  // ablation: no fp64 filter work, the decoded samples are summed
+        "fp64 filter bank removed: the 440 multiply-adds and adds per lane become 64 fp64 adds; "
+        "DMA, LDS reads and decode kept (wrong results)",
+        [("dwt8.h", FMA_BODY, """    (void)R;  // ablation: no fp64 filter work, the decoded samples are summed
     if (n == 0) {
-      for (int i = 0; i < 4; ++i) { U[i] = x1; V[i] = x0; W[i] = xs; }
-      P[8] = x1; P[9] = x0;
-    } else { U[n & 3] += x1; V[n & 3] += x0; }""")]),
+      for (int q = 0; q < 3; ++q) { A0[q] = x1; Ai[q] = x0; Bp[q] = xp; Bm[q] = xm; }
+    } else { A0[n % 3] += x1; Ai[n % 3] += x0; }""")]),
 }
 
 
