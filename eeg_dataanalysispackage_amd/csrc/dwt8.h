@@ -395,28 +395,29 @@ static __constant__ double kH5[kH5Size] = EEGFX_H5_TABLE;
 #define EEGFX_TOOM 1
 #endif
 
-template <typename Fetch>
-__device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
-                                                       int s, double& a6, double& d6) {
+// The core takes the samples through two callables: fetch(k) reads raw sample k of the lane's
+// slice (k < 64) and decode(v0, v1, x0, x1) turns the raw pair (k, k + 32) into doubles.
+template <typename Fetch, typename Decode>
+__device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, int gbase, int s,
+                                                    double& a6, double& d6) {
   typedef const __attribute__((address_space(4))) double* const_f64_ptr;
   const_f64_ptr tab = (const_f64_ptr)kH5;
   asm volatile("" : "+s"(tab));  // scalar loads of the table, not per-tap literal moves
-  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
   double P[10];  // P[j + 1]
 #if EEGFX_TOOM
   double A0[3], Ai[3], Bp[3], Bm[3];
   // the samples are fetched two pairs ahead of their use (the per-pair ordering below otherwise
   // leaves each pair's sample reads exposed)
-  typedef decltype(+fetch(0)) Raw;  // int for int16 samples (converted at use), float for float
+  typedef decltype(+fetch(0)) Raw;  // int for int16 samples (converted at use), float, double
   Raw vq[2][2];
 #pragma unroll
   for (int d = 0; d < 2; ++d) { vq[d][0] = fetch(d); vq[d][1] = fetch(d + 32); }
 #pragma unroll
   for (int n = 0; n < 32; ++n) {
-    const dwt8_f32x2 v = {(float)vq[n % 2][0], (float)vq[n % 2][1]};
+    const Raw v0 = vq[n % 2][0], v1 = vq[n % 2][1];
     if (n + 2 < 32) { vq[n % 2][0] = fetch(n + 2); vq[n % 2][1] = fetch(n + 2 + 32); }
-    const dwt8_f32x2 y = v * rr - bb;
-    const double x0 = (double)y.x, x1 = (double)y.y;
+    double x0, x1;
+    decode(v0, v1, x0, x1);
     const double xp = x1 + x0, xm = x1 - x0;  // exact: two floats
     const const_f64_ptr R = tab + n * kH5Cols;  // this pair's 12 constants (96 bytes)
 #pragma unroll
@@ -444,9 +445,8 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   // (without it the c3 kernel hoisted tap rows into SGPRs and spilled them to VGPR lanes)
 #pragma unroll
   for (int n = 0; n < 32; ++n) {
-    const dwt8_f32x2 v = {(float)fetch(n), (float)fetch(n + 32)};
-    const dwt8_f32x2 y = v * rr - bb;
-    const double x0 = (double)y.x, x1 = (double)y.y;
+    double x0, x1;
+    decode(fetch(n), fetch(n + 32), x0, x1);
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       if (n + 32 * j >= 280) continue;
@@ -470,6 +470,24 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
   halo<2, true>(a5, nullptr, gbase, s);
   a6 = fir10<true, false>(a5);
   d6 = fir10<true, true>(a5);
+}
+
+// The fused kernels' form: raw samples decoded as (double)((float)v * r - b), two correctly
+// rounded fp32 operations (DataProviderUtils.java:49-59, Baseline.java:39-41), a pair at a time
+// with packed fp32 math.
+template <typename Fetch>
+__device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
+                                                       int s, double& a6, double& d6) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  dwt8_collapsed_core(
+      fetch,
+      [&](auto v0, auto v1, double& x0, double& x1) {
+        const dwt8_f32x2 v = {(float)v0, (float)v1};
+        const dwt8_f32x2 y = v * rr - bb;
+        x0 = (double)y.x;
+        x1 = (double)y.y;
+      },
+      gbase, s, a6, d6);
 }
 
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps

@@ -86,50 +86,91 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
   }
 }
 
-// a11..a13 from materialised epochs.  A workgroup owns 8 epochs; wave w walks the channels
-// w, w+NW, ...; within a wave lane = 8*epoch + segment (dwt8.h).  Features are collected in LDS,
-// normalised per epoch with the reference's sequential sum of squares, and written coalesced.
+// a11..a13 from materialised epochs.  One wave per workgroup owns 8 epochs and walks their
+// channels; lane = 8*epoch + segment (dwt8.h).  For each channel the wave reads the 8 windows
+// (512 doubles each, contiguous in the epoch rows) with 16-byte loads, 1 KB of one window per
+// load instruction, and writes them to LDS in a bank-skewed layout: segment s of window g at
+// g*kFeWin + s*kFeSeg doubles.  kFeSeg = 65 doubles (130 dwords, 2 mod 64) and kFeWin = 520
+// (1,040 dwords, 16 mod 64), so the ds_read_b64 of lane (g, s) for any sample index falls on
+// banks 16g + 2s (+1) plus a common offset: the 32 lanes of a half-wave use 64 distinct banks.
+// (Each lane reading its own 512 contiguous bytes straight from memory touches 64 cache lines
+// per load instruction; that pattern moved ~1.9 TB/s.)  The filter bank then runs from LDS: FMA
+// the collapsed four-point filter of dwt8_collapsed_core on the doubles as they are, EXACT the
+// level-by-level cascade with value halos.  Features collect in LDS, are normalised per epoch
+// with the reference's sequential sum of squares and written coalesced.  33 KB of windows per
+// workgroup: 4 workgroups per CU.
+constexpr int kFeSeg = kSegLen + 1;
+constexpr int kFeWin = 8 * kFeSeg;
+typedef double f64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+
 template <bool FAST>
-__global__ __launch_bounds__(256) void features_from_epochs_kernel(const double* __restrict__ ep,
-                                                                   int64_t n, int C, int skip,
-                                                                   int nfeat, int row_stride,
-                                                                   double* __restrict__ out) {
+__global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* __restrict__ ep,
+                                                                  int64_t n, int C, int skip,
+                                                                  int nfeat, int row_stride,
+                                                                  double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) double win[8 * kFeWin];
   extern __shared__ __attribute__((aligned(16))) double fsmem[];
-  const int nw = blockDim.x / 64;
-  const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x;
   const int el = lane >> 3, s = lane & 7;
   const int F = C * nfeat;
-  double* xch = fsmem + w * 64 * kSlot;
-  double* feat = fsmem + nw * 64 * kSlot;  // [8][F]
-  double* norm = feat + 8 * F;            // [8]
+  double* feat = fsmem;         // [8][F]
+  double* norm = feat + 8 * F;  // [8]
   const int64_t e0 = (int64_t)blockIdx.x * 8;
-  const int64_t e = e0 + el;
-  const bool valid = e < n;
-  for (int c = w; c < C; c += nw) {
-    double x[kIn];
-    const double* src = ep + (valid ? (e * C + c) * row_stride + skip : 0);
+  const int64_t ne = (n - e0) < 8 ? (n - e0) : 8;
+  // quad q = 64 (j % 4) + lane of window j / 4: doubles 2q, 2q + 1 of segment q / 32.  Epochs
+  // past n read the last epoch's window (the loads stay unconditional; the result is dropped).
+  // Channel c + 1's windows are in flight while channel c runs the filter bank.
+  f64x2_a8 v[32];
+  auto load = [&](int c) {
 #pragma unroll
-    for (int k = 0; k < kIn; ++k) x[k] = valid ? src[(kSegLen * s + k) & (kWin - 1)] : 0.0;
+    for (int j = 0; j < 32; ++j) {
+      const int g = j >> 2;
+      const int64_t e = e0 + (g < ne ? g : ne - 1);
+      const int q = ((j & 3) << 6) | lane;
+      v[j] = *(const f64x2_a8*)(ep + (e * C + c) * row_stride + skip + 2 * q);
+    }
+  };
+  load(0);
+  for (int c = 0; c < C; ++c) {
+    wave_sync();  // the previous channel's LDS reads precede these writes
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int q = ((j & 3) << 6) | lane;
+      double* d = win + (j >> 2) * kFeWin + (q >> 5) * kFeSeg + 2 * (q & 31);
+      d[0] = v[j].x;
+      d[1] = v[j].y;
+    }
+    wave_sync();
+    if (c + 1 < C) load(c + 1);
+    const double* own = win + el * kFeWin + s * kFeSeg;
     double a6, d6;
-    dwt8_cascade<FAST>(x, xch, lane & ~7, s, a6, d6);
-    if (valid) {
+    if constexpr (FAST) {
+      dwt8_collapsed_core([&](int k) { return own[k]; },
+                          [](double v0, double v1, double& x0, double& x1) { x0 = v0; x1 = v1; },
+                          lane & ~7, s, a6, d6);
+    } else {
+      const double* sig = win + el * kFeWin;
+      double x[kIn];
+#pragma unroll
+      for (int k = 0; k < kIn; ++k) x[k] = k < kSegLen ? own[k] : sig[((s + 1) & 7) * kFeSeg + k - kSegLen];
+      dwt8_cascade<false, true>(x, nullptr, lane & ~7, s, a6, d6);
+    }
+    if (el < ne) {
       if (s < nfeat) feat[el * F + c * nfeat + s] = a6;
       if (8 + s < nfeat) feat[el * F + c * nfeat + 8 + s] = d6;
     }
   }
-  __syncthreads();
-  if (threadIdx.x < 8) {
+  wave_sync();
+  if (lane < ne) {
     double acc = 0.0;
     for (int i = 0; i < F; ++i) {
-      const double f = feat[threadIdx.x * F + i];
+      const double f = feat[lane * F + i];
       acc = acc + f * f;  // Math.pow(f, 2) summed in index order
     }
-    norm[threadIdx.x] = sqrt(acc);
+    norm[lane] = sqrt(acc);
   }
-  __syncthreads();
-  const int64_t ne = (n - e0) < 8 ? (n - e0) : 8;
-  for (int idx = threadIdx.x; idx < ne * F; idx += blockDim.x)
-    out[e0 * F + idx] = feat[idx] / norm[idx / F];
+  wave_sync();
+  for (int idx = lane; idx < ne * F; idx += 64) out[e0 * F + idx] = feat[idx] / norm[idx / F];
 }
 
 // a11..a13 for small host batches (the per-epoch IFeatureExtraction drop-in): one workgroup per
@@ -268,9 +309,8 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
                                        int nfeat, bool fast, double* out, int row_stride) {
   if (n == 0) return hipSuccess;
-  const int nw = C < 4 ? C : 4;
-  const size_t smem = sizeof(double) * ((size_t)nw * 64 * dev::kSlot + 8 * (size_t)C * nfeat + 8);
-  dim3 grid((unsigned)((n + 7) / 8)), block(64 * nw);
+  const size_t smem = sizeof(double) * (8 * (size_t)C * nfeat + 8);
+  dim3 grid((unsigned)((n + 7) / 8)), block(64);
   if (fast)
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
                        skip, nfeat, row_stride, out);
