@@ -86,6 +86,56 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
   }
 }
 
+// The same write pass for epochs of at most kCutPairs * 256 sample pairs (C <= 3): the channel
+// parameters and the epoch's baselines go to LDS first, and each thread issues the raw reads of
+// all its pairs before the first store, so a workgroup waits on memory twice instead of twice per
+// loop trip (3 channels: 7.3-7.4 -> 6.0-6.7 ms per 1M epochs, profiles/r03as/, r03au/).  Not used for wide
+// layouts: at 32 of 32 channels, whose sample reads lie 64 B apart, this form (with one pair per
+// trip) took 14.1 ms against 12.1 ms per 50k epochs (profiles/r03at/).
+constexpr int kCutPairs = 5;
+template <typename T>
+__global__ __launch_bounds__(256) void cut_write_small_kernel(
+    const T* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, double* __restrict__ out) {
+  __shared__ int s_col[kMaxChannels];
+  __shared__ float s_res[kMaxChannels], s_base[kMaxChannels];
+  const int t = threadIdx.x;
+  const int64_t e = blockIdx.x;
+  if (t < C) {
+    s_col[t] = sel.col[t];
+    s_res[t] = sel.res[t];
+    s_base[t] = base[e * C + t];
+  }
+  const int64_t p0 = pos[e];
+  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : kPre;  // flagged by the baselines
+  __syncthreads();
+  double* o = out + e * C * kPost;
+  const int npairs = C * (kPost / 2);  // <= 256 * kCutPairs (launcher)
+  float v0[kCutPairs], v1[kCutPairs];
+#pragma unroll
+  for (int u = 0; u < kCutPairs; ++u) {
+    const int idx = 256 * u + t;
+    v0[u] = v1[u] = 0.0f;
+    if (idx < npairs) {
+      const int c = idx / (kPost / 2);
+      const int64_t f = p + 2 * (idx - c * (kPost / 2));
+      const int col = s_col[c];
+      const float r = s_res[c];
+      // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
+      if (f >= 0 && f < n_frames) v0[u] = (float)raw[f * ct + col] * r;
+      if (f + 1 >= 0 && f + 1 < n_frames) v1[u] = (float)raw[(f + 1) * ct + col] * r;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kCutPairs; ++u) {
+    const int idx = 256 * u + t;
+    if (idx < npairs) {
+      const float b = s_base[idx / (kPost / 2)];
+      *(double2*)(o + 2 * idx) = make_double2((double)(v0[u] - b), (double)(v1[u] - b));
+    }
+  }
+}
+
 // a11..a13 from materialised epochs.  One wave per workgroup owns 8 epochs and walks their
 // channels; lane = 8*epoch + segment (dwt8.h).  For each channel the wave reads the 8 windows
 // (512 doubles each, contiguous in the epoch rows) with 16-byte loads, 1 KB of one window per
@@ -289,9 +339,16 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
   else if (scratch && baseline_any_supported(fmt, ct, C))
     be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err);
   if (be == hipSuccess) {
-    if (fmt == 0)
+    const bool small = C * (dev::kPost / 2) <= 256 * dev::kCutPairs;
+    if (fmt == 0 && small)
+      hipLaunchKernelGGL(dev::cut_write_small_kernel<int16_t>, grid, block, 0, st,
+                         (const int16_t*)raw, n_frames, ct, sel, C, pos, (const float*)scratch, out);
+    else if (fmt == 0)
       hipLaunchKernelGGL(dev::cut_write_kernel<int16_t>, grid, block, 0, st, (const int16_t*)raw,
                          n_frames, ct, sel, C, pos, (const float*)scratch, out);
+    else if (small)
+      hipLaunchKernelGGL(dev::cut_write_small_kernel<float>, grid, block, 0, st,
+                         (const float*)raw, n_frames, ct, sel, C, pos, (const float*)scratch, out);
     else
       hipLaunchKernelGGL(dev::cut_write_kernel<float>, grid, block, 0, st, (const float*)raw,
                          n_frames, ct, sel, C, pos, (const float*)scratch, out);

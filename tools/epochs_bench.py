@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--cut", action="store_true", help="also time eegfx_cut_epochs_f64")
     args = ap.parse_args()
     import torch
 
@@ -45,6 +46,35 @@ def main():
     ctx.synth_recording(raw, C, 7)
     pos = torch.arange(1000, 1000 * (n + 1), 1000, dtype=torch.int64, device=dev)
     ep = ctx.cut_epochs(raw, C, list(range(C)), [0.1] * C, pos)
+    if args.cut:  # getData(): the materialised epochs themselves (a3 + a5..a7)
+        for _ in range(args.warmup):
+            ctx.cut_epochs(raw, C, list(range(C)), [0.1] * C, pos, out=ep)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            ctx.cut_epochs(raw, C, list(range(C)), [0.1] * C, pos, out=ep)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.steps
+        bpe = 850 * C * 2 + 8 + 750 * C * 8  # frames read (as the reference cuts them) + rows out
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        for _ in range(args.steps):
+            ep.fill_(0.5)  # the write-bandwidth reference: the same rows, written only
+        f1.record(stream)
+        torch.cuda.synchronize(dev)
+        fill_ms = f0.elapsed_time(f1) / args.steps
+        ctx.cut_epochs(raw, C, list(range(C)), [0.1] * C, pos, out=ep)
+        torch.cuda.synchronize(dev)
+        print(json.dumps({"tool": "epochs_bench", "tag": args.tag, "op": "cut_epochs",
+                          "fill_ms": round(fill_ms, 4),
+                          "fill_GBps": round(ep.numel() * 8 / (fill_ms * 1e-3) / 1e9, 1),
+                          "epochs": n, "channels": C, "ms_per_call": round(ms, 4),
+                          "epochs_per_s": round(n / (ms * 1e-3), 1),
+                          "GBps_algorithmic": round(n * bpe / (ms * 1e-3) / 1e9, 1),
+                          "sha256_16": hashlib.sha256(ep.cpu().numpy().tobytes()).hexdigest()[:16]}),
+              flush=True)
     del raw
     out = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
     results = {}
