@@ -237,6 +237,12 @@ def main():
         else:
             args.epochs = 1_000_000
     n = args.epochs
+    if args.workload == "c3" and not distributed and n == 8_000_000:
+        wl = dict(WORKLOADS["c3dist"], desc="configs[2]: one rank's 8M-epoch shard on one GPU "
+                                            "(synthetic multiplexed int16, 3 ch @1000 Hz, 48 GB "
+                                            "recording) -> fe=dwt-8 48-dim L2-normalised features")
+    elif args.workload == "c3" and not distributed and n != 1_000_000:
+        wl = dict(wl, desc=wl["desc"].replace("1M epochs", f"{n} epochs (not the configs[1] size)"))
     sp = args.spacing
     if sp < 100:
         raise SystemExit("--spacing must be >= 100 frames")
