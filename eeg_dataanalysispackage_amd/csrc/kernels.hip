@@ -89,9 +89,9 @@ __global__ __launch_bounds__(256) void cut_write_kernel(const T* __restrict__ ra
 // The same write pass for epochs of at most kCutPairs * 256 sample pairs (C <= 3): the channel
 // parameters and the epoch's baselines go to LDS first, and each thread issues the raw reads of
 // all its pairs before the first store, so a workgroup waits on memory twice instead of twice per
-// loop trip (3 channels: 7.3-7.4 -> 6.0-6.7 ms per 1M epochs, profiles/r03as/, r03au/).  Not used for wide
-// layouts: at 32 of 32 channels, whose sample reads lie 64 B apart, this form (with one pair per
-// trip) took 14.1 ms against 12.1 ms per 50k epochs (profiles/r03at/).
+// loop trip (3 channels: 7.3-7.4 -> 6.0-6.7 ms per 1M epochs, profiles/r03as/, r03au/).  Since
+// the LDS-staged passes below (4.6 ms there, profiles/r03az/) it serves only the layouts they skip:
+// a few channels of a wide montage (ct > 8 C) or a raw buffer that is not dword aligned.
 constexpr int kCutPairs = 5;
 template <typename T>
 __global__ __launch_bounds__(256) void cut_write_small_kernel(
@@ -133,6 +133,156 @@ __global__ __launch_bounds__(256) void cut_write_small_kernel(
       const float b = s_base[idx / (kPost / 2)];
       *(double2*)(o + 2 * idx) = make_double2((double)(v0[u] - b), (double)(v1[u] - b));
     }
+  }
+}
+
+// The LDS-staged write pass for frames of a whole number of dwords (e.g. configs[3]'s 32-channel
+// montage; used while the staged frames are at most twice the rows written, ct <= 8 C for int16).
+// Reading one channel's samples straight from the multiplexed recording puts consecutive lanes a
+// whole frame (64 B at 32 int16 channels) apart, so each wave load touches 64 cache lines for 128
+// useful bytes (11.9 ms per 50k 32-channel epochs, 1.0 TB/s, profiles/r03at/).  Here workgroup
+// (e, chunk) copies frames [f0, f0 + nf) of epoch e's post-stimulus span into LDS with coalesced
+// dword loads, one padding dword per frame (frame stride FW + 1 dwords: odd when FW is even, so 64
+// lanes reading 64 frames of one channel hit 64 distinct banks), then each lane decodes two
+// consecutive samples of one channel row and stores them as one 16-byte pair: 3.14 ms
+// (profiles/r03az/; 16-byte staging loads measured the same).  Frames past the recording's end
+// read as 0.0f (Arrays.copyOfRange zero padding).
+constexpr int kCutLdsMax = 32 * 1024;
+template <typename T>
+__global__ __launch_bounds__(256) void cut_write_lds_kernel(
+    const T* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, double* __restrict__ out,
+    int nfc) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
+  __shared__ int s_col[kMaxChannels];
+  __shared__ float s_res[kMaxChannels], s_base[kMaxChannels];
+  const int t = threadIdx.x;
+  const int64_t e = blockIdx.x;
+  const int f0 = (int)blockIdx.y * nfc;
+  const int nf = kPost - f0 < nfc ? kPost - f0 : nfc;  // even: nfc and kPost are
+  if (t < C) {
+    s_col[t] = sel.col[t];
+    s_res[t] = sel.res[t];
+    s_base[t] = base[e * C + t];
+  }
+  const int64_t p0 = pos[e];
+  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : kPre;  // flagged by the baselines
+  const int FW = ct * (int)sizeof(T) / 4, FS = FW + 1;
+  const int64_t g0 = p + f0;  // first frame of this chunk
+  const uint32_t* src = (const uint32_t*)raw;
+  {  // dword k of the chunk is (frame k / FW, word k % FW); 8 loads in flight per thread
+    const int total = nf * FW, sf = 256 / FW, sw = 256 % FW;
+    int f = t / FW, w = t - (t / FW) * FW;
+    for (int k0 = 0; k0 < total; k0 += 8 * 256) {
+      uint32_t v[8];
+      int fk[8], wk[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        fk[u] = f;
+        wk[u] = w;
+        const bool in = k0 + 256 * u + t < total && g0 + f < n_frames;
+        v[u] = in ? src[(g0 + f) * FW + w] : 0u;
+        f += sf;
+        w += sw;
+        if (w >= FW) { w -= FW; ++f; }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + 256 * u + t < total) stage[fk[u] * FS + wk[u]] = v[u];
+    }
+  }
+  __syncthreads();
+  // rows: pair q of channel c covers frames f0 + 2q, f0 + 2q + 1
+  const int hp = nf / 2, npairs = C * hp, sc = 256 / hp, sq = 256 % hp;
+  int c = t / hp, q = t - (t / hp) * hp;
+  double* o = out + e * C * kPost + f0;
+  for (int idx = t; idx < npairs; idx += 256) {
+    const int col = s_col[c];
+    const float r = s_res[c], b = s_base[c];
+    const int f = 2 * q;
+    float s0, s1;
+    if constexpr (sizeof(T) == 2) {
+      const int16_t* h = (const int16_t*)stage;
+      s0 = (float)h[2 * f * FS + col];
+      s1 = (float)h[2 * (f + 1) * FS + col];
+    } else {
+      const float* h = (const float*)stage;
+      s0 = h[f * FS + col];
+      s1 = h[(f + 1) * FS + col];
+    }
+    // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
+    const float v0 = g0 + f < n_frames ? s0 * r : 0.0f;
+    const float v1 = g0 + f + 1 < n_frames ? s1 * r : 0.0f;
+    *(double2*)(o + (int64_t)c * kPost + f) = make_double2((double)(v0 - b), (double)(v1 - b));
+    c += sc;
+    q += sq;
+    if (q >= hp) { q -= hp; ++c; }
+  }
+}
+
+// The same LDS-staged write pass for int16 frames that are not a whole number of dwords (the
+// 3-channel path of configs[0]-[2]: 6-byte frames): the chunk's bytes are staged as they lie, from
+// the dword that holds its first frame, without per-frame padding; lanes reading the sample pairs
+// of one channel are 2 frames apart (3 dwords at 3 channels: an odd stride, no bank conflicts).
+// The dword holding the recording's last two bytes is read as a half so no load passes its end.
+__global__ __launch_bounds__(256) void cut_write_lds_packed_kernel(
+    const int16_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, double* __restrict__ out,
+    int nfc) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
+  __shared__ int s_col[kMaxChannels];
+  __shared__ float s_res[kMaxChannels], s_base[kMaxChannels];
+  const int t = threadIdx.x;
+  const int64_t e = blockIdx.x;
+  const int f0 = (int)blockIdx.y * nfc;
+  const int nf = kPost - f0 < nfc ? kPost - f0 : nfc;
+  if (t < C) {
+    s_col[t] = sel.col[t];
+    s_res[t] = sel.res[t];
+    s_base[t] = base[e * C + t];
+  }
+  const int64_t p0 = pos[e];
+  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : kPre;  // flagged by the baselines
+  const int64_t g0 = p + f0;
+  const int FB = 2 * ct;
+  const int64_t nbytes = n_frames * FB;
+  const int64_t b0 = g0 * FB;                 // first byte of the chunk
+  const int64_t a0 = b0 >> 2;                 // its dword
+  const int delta = (int)(b0 & 3);            // 0 or 2
+  const int total = (delta + nf * FB + 3) >> 2;
+  const uint32_t* src = (const uint32_t*)raw;
+  for (int k0 = 0; k0 < total; k0 += 8 * 256) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 256 * u + t;
+      const int64_t a = (a0 + k) * 4;
+      v[u] = 0u;
+      if (k < total) {
+        if (a + 4 <= nbytes) v[u] = src[a0 + k];
+        else if (a + 2 <= nbytes) v[u] = (uint16_t)raw[(a >> 1)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + 256 * u + t < total) stage[k0 + 256 * u + t] = v[u];
+  }
+  __syncthreads();
+  const int16_t* h = (const int16_t*)((const uint8_t*)stage + delta);
+  const int hp = nf / 2, npairs = C * hp, sc = 256 / hp, sq = 256 % hp;
+  int c = t / hp, q = t - (t / hp) * hp;
+  double* o = out + e * C * kPost + f0;
+  for (int idx = t; idx < npairs; idx += 256) {
+    const int col = s_col[c];
+    const float r = s_res[c], b = s_base[c];
+    const int f = 2 * q;
+    // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
+    const float v0 = g0 + f < n_frames ? (float)h[f * ct + col] * r : 0.0f;
+    const float v1 = g0 + f + 1 < n_frames ? (float)h[(f + 1) * ct + col] * r : 0.0f;
+    *(double2*)(o + (int64_t)c * kPost + f) = make_double2((double)(v0 - b), (double)(v1 - b));
+    c += sc;
+    q += sq;
+    if (q >= hp) { q -= hp; ++c; }
   }
 }
 
@@ -340,7 +490,34 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
     be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err);
   if (be == hipSuccess) {
     const bool small = C * (dev::kPost / 2) <= 256 * dev::kCutPairs;
-    if (fmt == 0 && small)
+    const int fbytes = ct * (fmt == 0 ? 2 : 4);
+    // LDS staging reads every byte of the epoch's frames: used while they are at most twice the
+    // rows written (ct <= 8 C int16), so a few channels of a wide montage keep the direct reads
+    const bool stage = ((uintptr_t)raw & 3) == 0 && (int64_t)dev::kPost * fbytes <= 2 * 6000LL * C;
+    if (stage && fbytes % 4 != 0 && fmt == 0) {
+      const int nch = (dev::kPost * fbytes + 8 + dev::kCutLdsMax - 1) / dev::kCutLdsMax;
+      const int nfc = ((dev::kPost + nch - 1) / nch + 1) & ~1;
+      const int nchunks = (dev::kPost + nfc - 1) / nfc;
+      dim3 g2((unsigned)n, (unsigned)nchunks);
+      hipLaunchKernelGGL(dev::cut_write_lds_packed_kernel, g2, block, (size_t)nfc * fbytes + 8, st,
+                         (const int16_t*)raw, n_frames, ct, sel, C, pos, (const float*)scratch,
+                         out, nfc);
+    } else if (stage && fbytes % 4 == 0) {
+      // wide layouts: LDS-staged chunks of the epoch, an even number of frames each
+      const int fs_bytes = (fbytes / 4 + 1) * 4;
+      const int nch = (dev::kPost * fs_bytes + dev::kCutLdsMax - 1) / dev::kCutLdsMax;
+      const int nfc = ((dev::kPost + nch - 1) / nch + 1) & ~1;
+      const int nchunks = (dev::kPost + nfc - 1) / nfc;
+      dim3 g2((unsigned)n, (unsigned)nchunks);
+      const size_t lds = (size_t)nfc * fs_bytes;
+      if (fmt == 0)
+        hipLaunchKernelGGL(dev::cut_write_lds_kernel<int16_t>, g2, block, lds, st,
+                           (const int16_t*)raw, n_frames, ct, sel, C, pos, (const float*)scratch,
+                           out, nfc);
+      else
+        hipLaunchKernelGGL(dev::cut_write_lds_kernel<float>, g2, block, lds, st, (const float*)raw,
+                           n_frames, ct, sel, C, pos, (const float*)scratch, out, nfc);
+    } else if (fmt == 0 && small)
       hipLaunchKernelGGL(dev::cut_write_small_kernel<int16_t>, grid, block, 0, st,
                          (const int16_t*)raw, n_frames, ct, sel, C, pos, (const float*)scratch, out);
     else if (fmt == 0)

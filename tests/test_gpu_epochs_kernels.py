@@ -92,3 +92,39 @@ def test_device_cut_epochs_small_and_wide(ctxs, fmt, cols):
                            torch.from_numpy(pos.astype(np.int64)).cuda())
     exact.synchronize()
     assert eq(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("fmt,ct,cols", [
+    ("int16", 32, list(range(32))),           # configs[3]'s montage: 16 dwords per frame
+    ("int16", 32, [31, 0, 7, 16, 3]),         # a few of many channels, any order
+    ("int16", 8, [7, 6, 5, 4, 3, 2, 1, 0]),   # 4 dwords per frame
+    ("int16", 6, [0, 2, 4, 5]),               # odd dword count per frame (even LDS stride)
+    ("int16", 3, [0, 1, 2]),                  # 6-byte frames: the packed staging (configs[1])
+    ("int16", 3, [2, 0]),
+    ("int16", 7, [3]),                        # 14-byte frames, one channel of seven
+    ("float32", 32, list(range(0, 32, 2))),   # 32 dwords per frame: four chunks per epoch
+    ("float32", 5, [4, 3, 2, 1, 0]),
+])
+def test_device_cut_epochs_lds_staged(ctxs, fmt, ct, cols):
+    """getData() with the LDS-staged write passes (the epoch's frames at most twice the rows):
+    cut_write_lds_kernel for whole-dword frames (padded per frame, in chunks),
+    cut_write_lds_packed_kernel for int16 frames that are not (staged as they lie); rows written as
+    16-byte pairs.  Value-equal to the oracle's decode (OffLineDataProvider.java:216-233), markers at
+    pos = 100 and past the end of the recording (zero padding, Arrays.copyOfRange)."""
+    import torch
+    rng = np.random.default_rng(ct * 100 + len(cols))
+    nf = 12_001  # odd: with an odd channel count the recording ends inside a dword
+    if fmt == "int16":
+        raw = np.clip(rng.integers(-26000, -24000, size=(1, ct)) +
+                      np.cumsum(rng.integers(-40, 41, size=(nf, ct)), axis=0),
+                      -32768, 32767).astype(np.int16)
+    else:
+        raw = (rng.standard_normal((nf, ct)) * 50.0).astype(np.float32)
+    pos = np.concatenate([[100], rng.integers(100, nf, size=21), [nf - 749, nf - 400, nf, nf + 100]])
+    res = list(rng.choice([0.1, 0.25, 1.0, 0.5, 0.048828125], size=len(cols)))
+    want = oracle.decode_epochs(raw, cols, res, pos)
+    exact, _ = ctxs
+    got = exact.cut_epochs(torch.from_numpy(raw).cuda(), ct, cols, res,
+                           torch.from_numpy(pos.astype(np.int64)).cuda())
+    exact.synchronize()
+    assert eq(got.cpu().numpy(), want)
