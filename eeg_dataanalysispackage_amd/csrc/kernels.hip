@@ -144,10 +144,17 @@ __global__ __launch_bounds__(256) void cut_write_small_kernel(
 // (e, chunk) copies frames [f0, f0 + nf) of epoch e's post-stimulus span into LDS with coalesced
 // dword loads, one padding dword per frame (frame stride FW + 1 dwords: odd when FW is even, so 64
 // lanes reading 64 frames of one channel hit 64 distinct banks), then each lane decodes two
-// consecutive samples of one channel row and stores them as one 16-byte pair: 3.14 ms
-// (profiles/r03az/; 16-byte staging loads measured the same).  Frames past the recording's end
+// consecutive samples of one channel row and stores them as one 16-byte pair: 2.3 ms
+// (profiles/r03bc/; 16-byte staging loads measured the same as dword loads, profiles/r03az/).  Frames past the recording's end
 // read as 0.0f (Arrays.copyOfRange zero padding).
-constexpr int kCutLdsMax = 32 * 1024;
+// Chunk size: one chunk per epoch up to 64 KB of LDS (32 int16 channels: 51 KB, 3 workgroups per
+// CU) -- each workgroup's rows are then one contiguous 192 KB run.  Chunks of 12 / 16 / 32 KB
+// (more workgroups per CU, rows written in pieces) took 3.71 / 3.54 / 3.14 ms against 2.30-2.33 ms
+// for 50k 32-channel epochs, C = 3 unchanged (profiles/r03bc/ab.log; -DEEGFX_CUT_LDS_MAX builds).
+#ifndef EEGFX_CUT_LDS_MAX
+#define EEGFX_CUT_LDS_MAX (64 * 1024)
+#endif
+constexpr int kCutLdsMax = EEGFX_CUT_LDS_MAX;
 template <typename T>
 __global__ __launch_bounds__(256) void cut_write_lds_kernel(
     const T* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
