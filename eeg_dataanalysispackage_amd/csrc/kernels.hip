@@ -482,6 +482,14 @@ __global__ __launch_bounds__(256) void synth_kernel(int16_t* __restrict__ dst, i
 }  // namespace dev
 
 // ---- launchers ---------------------------------------------------------------------------------
+// Frames per LDS chunk of the staged getData passes: an even count, the 750 frames split into as
+// few chunks as keep each chunk's LDS (frame_bytes per frame + slack) within kCutLdsMax.
+static int cut_chunk_frames(int frame_bytes, int slack) {
+  for (int nch = 1;; ++nch) {
+    const int nfc = ((dev::kPost + nch - 1) / nch + 1) & ~1;
+    if ((int64_t)nfc * frame_bytes + slack <= dev::kCutLdsMax || nfc <= 2) return nfc;
+  }
+}
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                              double* out, void* scratch, int* err) {
@@ -502,8 +510,7 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
     // rows written (ct <= 8 C int16), so a few channels of a wide montage keep the direct reads
     const bool stage = ((uintptr_t)raw & 3) == 0 && (int64_t)dev::kPost * fbytes <= 2 * 6000LL * C;
     if (stage && fbytes % 4 != 0 && fmt == 0) {
-      const int nch = (dev::kPost * fbytes + 8 + dev::kCutLdsMax - 1) / dev::kCutLdsMax;
-      const int nfc = ((dev::kPost + nch - 1) / nch + 1) & ~1;
+      const int nfc = cut_chunk_frames(fbytes, 8);
       const int nchunks = (dev::kPost + nfc - 1) / nfc;
       dim3 g2((unsigned)n, (unsigned)nchunks);
       hipLaunchKernelGGL(dev::cut_write_lds_packed_kernel, g2, block, (size_t)nfc * fbytes + 8, st,
@@ -512,8 +519,7 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
     } else if (stage && fbytes % 4 == 0) {
       // wide layouts: LDS-staged chunks of the epoch, an even number of frames each
       const int fs_bytes = (fbytes / 4 + 1) * 4;
-      const int nch = (dev::kPost * fs_bytes + dev::kCutLdsMax - 1) / dev::kCutLdsMax;
-      const int nfc = ((dev::kPost + nch - 1) / nch + 1) & ~1;
+      const int nfc = cut_chunk_frames(fs_bytes, 0);
       const int nchunks = (dev::kPost + nfc - 1) / nfc;
       dim3 g2((unsigned)n, (unsigned)nchunks);
       const size_t lds = (size_t)nfc * fs_bytes;
