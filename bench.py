@@ -95,6 +95,9 @@ def parse():
                     help="epochs in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather legs")
+    ap.add_argument("--trace-steps", action="store_true",
+                    help="study only: device time of every warmup and timed step (HIP events "
+                         "between steps), reported under 'step_trace'")
     ap.add_argument("--gather-timeout", type=float, default=300.0,
                     help="seconds the gather legs may take before rank 0 reports the extraction "
                          "line without them and every rank exits")
@@ -263,8 +266,21 @@ def main():
     def step():
         ctx.process_recording(raw, ct, cols, res, pos, out=out)
 
-    for _ in range(args.warmup):
-        step()
+    trace = {"warmup": [], "timed": []} if args.trace_steps else None
+
+    def traced(k, key):
+        if trace is None:
+            for _ in range(k):
+                step()
+            return
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)]
+        evs[0].record(stream)
+        for i in range(k):
+            step()
+            evs[i + 1].record(stream)
+        trace[key] = evs
+
+    traced(args.warmup, "warmup")
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -275,8 +291,7 @@ def main():
     ctx.set_timing(True)  # HIP events around each window_kernel launch, on the context stream
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        step()
+    traced(args.steps, "timed")
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if distributed:
@@ -388,6 +403,9 @@ def main():
 
     if line is not None and alt:
         line["alt_numerics"] = alt
+    if line is not None and trace is not None:
+        line["step_trace"] = {k: [round(a.elapsed_time(b), 4) for a, b in zip(v, v[1:])]
+                              for k, v in trace.items()}
 
     # The gathers are the first RCCL traffic between the ranks' own communicators; a hang there
     # must not cost the extraction line (or keep every rank alive until the launcher's limit).

@@ -141,6 +141,14 @@ class Context:
                                            ctypes.byref(by)))
         return int(n.value), float(ms.value), int(by.value)
 
+    def guard_stats(self, reset: bool = False):
+        """(rows checked, rows recomputed under EXACT) of the fma numerics' conditioning guard
+        since the context was created or last reset (eegfx_ctx_guard_stats; synchronises)."""
+        a, b = c_int64(), c_int64()
+        check(lib().eegfx_ctx_guard_stats(self.handle, ctypes.byref(a), ctypes.byref(b),
+                                          1 if reset else 0))
+        return int(a.value), int(b.value)
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
             lib().eegfx_ctx_destroy(self._h)

@@ -149,12 +149,26 @@ struct eegfx_ctx {
   DevBuf raw, pos, out, scratch, fused;
   DevBuf lr_x, lr_y, lr_state, lr_part;  // logistic regression (eegfx_logreg_*)
   PinBuf pin_in, pin_out;                // small-batch extract_features staging (zero-copy)
+  // The fma numerics' conditioning guard (guard.h): a device word pair (the flagged-row count of
+  // the current launch, then the running total of recomputed rows) and the flagged-row list;
+  // guard_checked counts the rows that went through a guarded launch.
+  int* guard_dev = nullptr;
+  DevBuf guard_list;
+  int64_t guard_checked = 0;
+  Guard guard_for(int64_t n) {
+    if (numerics == EEGFX_EXACT) return Guard{nullptr, nullptr, nullptr};
+    guard_checked += n;
+    return Guard{guard_dev, (int64_t*)guard_list.get(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1)),
+                 (unsigned long long*)(guard_dev + 2)};
+  }
   void bind_buffers() {
-    for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part})
+    for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
+                      &guard_list})
       b->sp = &stream;
   }
   void release_buffers() {
-    for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part})
+    for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
+                      &guard_list})
       b->release();
     pin_in.release();
     pin_out.release();
@@ -290,25 +304,32 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
                            const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                            double* out) {
   const bool fast = ctx->numerics != EEGFX_EXACT;
+  // fma: rows that fail the conditioning guard are recomputed under EXACT by a follow-up launch
+  // (guard.h, guard.hip); the baseline kernel zeroes the guard count
+  const Guard g = ctx->guard_for(n);
   if (fused_supported(fmt, ct, C, out)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch,
-                                    ctx->err_dev));
+                                    ctx->err_dev, g.count));
     ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
     HIP_CHECK(launch_fused_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fast, fscratch,
-                                  out));
+                                  out, g));
     ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
+    HIP_CHECK(launch_guard_fixup_raw(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, fscratch, g,
+                                     out));
     return;
   }
   if (wide_supported(fmt, ct, C)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_baseline_any(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fscratch,
-                                  ctx->err_dev));
+                                  ctx->err_dev, g.count));
     ctx->tic();
     HIP_CHECK(launch_window_wide(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast,
-                                 fscratch, out));
+                                 fscratch, out, g));
     const int64_t elem = fmt == EEGFX_INT_16 ? 2 : 4;
     ctx->toc(n * (EEGFX_DWT8_EPOCH_SIZE * ct * elem + C * 4 + 8 + C * 16 * 8));
+    HIP_CHECK(launch_guard_fixup_raw(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, fscratch, g,
+                                     out));
     return;
   }
   double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
@@ -316,8 +337,10 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep,
                               ctx->fused.get(fused_scratch_bytes(n, C)), ctx->err_dev));
   HIP_CHECK(launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
-                                        EEGFX_DWT8_FEATURE_SIZE, fast, out));
+                                        EEGFX_DWT8_FEATURE_SIZE, fast, out, EEGFX_POSTSTIMULUS, g));
   ctx->toc(0);
+  HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, ep, C, EEGFX_DWT8_SKIP, EEGFX_DWT8_FEATURE_SIZE,
+                                      EEGFX_POSTSTIMULUS, g, out));
 }
 
 }  // namespace
@@ -571,6 +594,8 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     HIP_CHECK(hipHostMalloc((void**)&c->err_host, sizeof(int), hipHostMallocMapped));
     *c->err_host = 0;
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
+    HIP_CHECK(hipMalloc((void**)&c->guard_dev, 16));
+    HIP_CHECK(hipMemset(c->guard_dev, 0, 16));
     *out = c.release();
   });
 }
@@ -621,6 +646,25 @@ int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
   });
 }
 
+int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_recomputed,
+                          int reset) {
+  return guarded([&] {
+    if (!ctx || !rows_checked || !rows_recomputed) fail(EEGFX_EINVAL, "null argument");
+    ctx->activate();
+    unsigned long long total = 0;
+    HIP_CHECK(hipMemcpyAsync(&total, ctx->guard_dev + 2, sizeof(total), hipMemcpyDeviceToHost,
+                             ctx->stream));
+    ctx->drain();
+    *rows_checked = ctx->guard_checked;
+    *rows_recomputed = (int64_t)total;
+    if (reset) {
+      HIP_CHECK(hipMemsetAsync(ctx->guard_dev + 2, 0, sizeof(total), ctx->stream));
+      ctx->drain();
+      ctx->guard_checked = 0;
+    }
+  });
+}
+
 int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,
                            int64_t* total_bytes) {
   return guarded([&] {
@@ -649,6 +693,7 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->own);
     if (ctx->err_host) (void)hipHostFree(ctx->err_host);
+    if (ctx->guard_dev) (void)hipFree(ctx->guard_dev);
     ctx->release_stream_resources();
     ctx->destroy_events();
     (void)hipStreamDestroy(ctx->own);
@@ -742,7 +787,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         ctx->tic();
         HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
                                         feature_size, ctx->numerics != EEGFX_EXACT,
-                                        (double*)ctx->pin_out.device_ptr()));
+                                        (double*)ctx->pin_out.device_ptr(), ctx->guard_for(n)));
         ctx->toc(0);
         ctx->wait_small();
         ctx->check_positions_flag();
@@ -758,15 +803,18 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
       const size_t chunk_bytes = (size_t)std::min<int64_t>(n, kChunk) * C * row_w;
       uint8_t* dwin = (uint8_t*)ctx->scratch.get(chunk_bytes);
       double* d_out = (double*)ctx->out.get(out_bytes);
+      const Guard g = ctx->guard_for(n);
       ctx->tic();
       for (int64_t e0 = 0; e0 < n; e0 += kChunk) {
         const int64_t m = std::min<int64_t>(kChunk, n - e0);
         HIP_CHECK(hipMemcpy2DAsync(dwin, row_w, src + (size_t)e0 * C * row_p, row_p, row_w,
                                    (size_t)(m * C), hipMemcpyHostToDevice, ctx->stream));
+        double* rows = d_out + e0 * C * feature_size;
         HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)dwin, m, C, 0,
-                                              feature_size, ctx->numerics != EEGFX_EXACT,
-                                              d_out + e0 * C * feature_size,
-                                              EEGFX_DWT8_EPOCH_SIZE));
+                                              feature_size, ctx->numerics != EEGFX_EXACT, rows,
+                                              EEGFX_DWT8_EPOCH_SIZE, g));
+        HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, (const double*)dwin, C, 0, feature_size,
+                                            EEGFX_DWT8_EPOCH_SIZE, g, rows));
       }
       ctx->toc(0);
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -775,10 +823,14 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
     }
     const double* d_in = (const double*)stage_in(ctx, ctx->scratch, epochs, in_bytes, mem);
     double* d_out = mem == EEGFX_MEM_DEVICE ? out : (double*)ctx->out.get(out_bytes);
+    const Guard g = ctx->guard_for(n);
     ctx->tic();
     HIP_CHECK(launch_features_from_epochs(ctx->stream, d_in, n, C, skip, feature_size,
-                                          ctx->numerics != EEGFX_EXACT, d_out));
+                                          ctx->numerics != EEGFX_EXACT, d_out, EEGFX_POSTSTIMULUS,
+                                          g));
     ctx->toc(0);
+    HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, d_in, C, skip, feature_size,
+                                        EEGFX_POSTSTIMULUS, g, d_out));
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       ctx->drain();
@@ -1193,9 +1245,13 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
     ctx->activate();
     const size_t out_bytes = sizeof(double) * (size_t)odp->n_epochs * 3 * feature_size;
     double* d_out = (double*)ctx->out.get(out_bytes);
+    const Guard g = ctx->guard_for(odp->n_epochs);
     HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)odp->d_epochs,
                                           odp->n_epochs, 3, skip, feature_size,
-                                          ctx->numerics != EEGFX_EXACT, d_out));
+                                          ctx->numerics != EEGFX_EXACT, d_out, EEGFX_POSTSTIMULUS,
+                                          g));
+    HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, (const double*)odp->d_epochs, 3, skip,
+                                        feature_size, EEGFX_POSTSTIMULUS, g, d_out));
     HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     ctx->drain();
   });

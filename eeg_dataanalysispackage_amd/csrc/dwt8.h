@@ -475,19 +475,37 @@ __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, 
 // The fused kernels' form: raw samples decoded as (double)((float)v * r - b), two correctly
 // rounded fp32 operations (DataProviderUtils.java:49-59, Baseline.java:39-41), a pair at a time
 // with packed fp32 math.
-template <typename Fetch>
+// TRACK: also returns in `ymax` the largest |x| of the lane's 64 samples (the guard's measured X
+// for float32 recordings, guard.h).
+template <bool TRACK = false, typename Fetch>
 __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, float b, int gbase,
-                                                       int s, double& a6, double& d6) {
+                                                       int s, double& a6, double& d6,
+                                                       float* ymax = nullptr) {
   const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  float m = 0.0f;
   dwt8_collapsed_core(
       fetch,
       [&](auto v0, auto v1, double& x0, double& x1) {
         const dwt8_f32x2 v = {(float)v0, (float)v1};
         const dwt8_f32x2 y = v * rr - bb;
+        if constexpr (TRACK) m = fmaxf(m, fmaxf(fabsf(y.x), fabsf(y.y)));
         x0 = (double)y.x;
         x1 = (double)y.y;
       },
       gbase, s, a6, d6);
+  if constexpr (TRACK) *ymax = m;
+}
+
+// The largest value of v over the 8 lanes of a signal group.
+__device__ __forceinline__ float group8_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1, 64));
+  v = fmaxf(v, __shfl_xor(v, 2, 64));
+  return fmaxf(v, __shfl_xor(v, 4, 64));
+}
+__device__ __forceinline__ double group8_max(double v) {
+  v = fmax(v, __shfl_xor(v, 1, 64));
+  v = fmax(v, __shfl_xor(v, 2, 64));
+  return fmax(v, __shfl_xor(v, 4, 64));
 }
 
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps

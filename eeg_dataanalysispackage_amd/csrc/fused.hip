@@ -39,6 +39,7 @@
 #include <cstdint>
 
 #include "dwt8.h"
+#include "guard.h"
 #include "launch.h"
 #include "lds_dma.h"
 
@@ -139,7 +140,8 @@ __device__ __forceinline__ void flag_position(int* err) {
 template <int CT, int C, int TILE, bool STREAM = false>
 __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
-    int64_t n, float* __restrict__ bout, int64_t* __restrict__ wout, int* __restrict__ err) {
+    int64_t n, float* __restrict__ bout, int64_t* __restrict__ wout, int* __restrict__ err,
+    int* __restrict__ guard_count) {
   using G = Geometry<CT>;
   constexpr int NT = (TILE * C + 63) / 64 * 64;
   __shared__ __attribute__((aligned(16))) uint32_t stage[TILE * G::BSTR];
@@ -148,6 +150,8 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   const int64_t nbytes = n_frames * G::FB;
   const int64_t t0 = (int64_t)blockIdx.x * TILE;
   const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
+  // the window kernel that follows appends to the guard list (fma numerics)
+  if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
   if (tid < TILE) {
     const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
     if (!position_ok(p, n_frames)) flag_position(err);
@@ -231,10 +235,14 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
 //          butterfly completes the row sum, and the row is scaled by 1/sqrt (rsqrt_nr: within an
 //          ulp or two of x / s; an all-zero row still gives NaN = 0 * inf); the scaled rows go
 //          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
-//          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).
-template <int F, bool FAST>
+//          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).  A row
+//          whose sum of squares fails the conditioning guard (guard.h; gx = the C per-signal X^2)
+//          is appended to the guard list for the EXACT follow-up launch.
+template <int F, bool FAST, int C = F / 16>
 __device__ __forceinline__ void normalise_store(double* fb, double* norm, double* o, int ne,
-                                                int lane) {
+                                                int lane, const double* gx = nullptr,
+                                                Guard g = Guard{nullptr, nullptr, nullptr},
+                                                int64_t e0 = 0) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   if constexpr (FAST) {
     static_assert(F % 16 == 0, "8 lanes per row, pairs of features");
@@ -250,6 +258,12 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
+    if (g.count && p == 0 && e < ne) {
+      double sx = 0.0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) sx += gx[e * C + c];
+      if (guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(g, e0 + e);
+    }
     const double inv = rsqrt_nr(acc);
     if (e < ne) {
 #pragma unroll
@@ -379,12 +393,13 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 template <int CT, int C, bool FAST, bool NT>
 __global__ __launch_bounds__(64 * C, 5) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
-    const float* __restrict__ base, int64_t n, double* __restrict__ out) {
+    const float* __restrict__ base, int64_t n, double* __restrict__ out, Guard guard) {
   using G = Geometry<CT>;
   constexpr int F = C * 16;
   static_assert(kSub * F * 8 <= kSub * G::ESTR * 4, "feature rows alias the window buffer");
   __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
   __shared__ double norm[kSub];
+  __shared__ double gx[FAST ? kSub * C : 1];  // the guard's X^2 per signal (fma numerics)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int el = lane >> 3, s = lane & 7;
@@ -398,6 +413,7 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   const bool mine = el < ne;
   const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
   const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
+  if (FAST && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
   const DmaRows<CT> rows(lane);
   if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
     dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
@@ -421,7 +437,8 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   fb[slot] = a6;
   fb[slot + 8] = d6;
   __syncthreads();
-  if (w == 0) normalise_store<F, FAST>(fb, norm, out + e0 * F, ne, lane);
+  if (w == 0)
+    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, e0);
 }
 
 }  // namespace dev
@@ -454,7 +471,7 @@ int64_t fused_window_bytes_per_epoch(int ct, int C) {
 
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 void* scratch, int* err) {
+                                 void* scratch, int* err, int* guard_count) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
   // 64 epochs per workgroup; 16/32/128 measured the same or slower.  Streaming
@@ -463,16 +480,17 @@ hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_fram
   int64_t* words = (int64_t*)((uint8_t*)scratch + window_words_offset(n, C));
   if (streaming_reads(n_frames, n, dev::kPre + 687))
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,
-                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, words, err);
+                       (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, words, err,
+                       guard_count);
   else
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,
-                       n_frames, sel, pos, n, (float*)scratch, words, err);
+                       n_frames, sel, pos, n, (float*)scratch, words, err, guard_count);
   return hipGetLastError();
 }
 
 hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                               const void* scratch, double* out) {
+                               const void* scratch, double* out, const Guard& guard) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
   const float* bs = (const float*)scratch;
@@ -482,7 +500,7 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
   const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
 #define EEGFX_WIN(FA, NTV)                                                                         \
   hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192), 0, st, (const uint8_t*)raw, \
-                     n_frames, sel, words, bs, n, out)
+                     n_frames, sel, words, bs, n, out, guard)
   if (fast) { if (nt) EEGFX_WIN(true, true); else EEGFX_WIN(true, false); }
   else { if (nt) EEGFX_WIN(false, true); else EEGFX_WIN(false, false); }
 #undef EEGFX_WIN

@@ -12,8 +12,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "dwt8.h"
+#include "guard.h"
 #include "launch.h"
 
 namespace eegfx {
@@ -310,11 +312,14 @@ constexpr int kFeSeg = kSegLen + 1;
 constexpr int kFeWin = 8 * kFeSeg;
 typedef double f64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
 
+// Under fma numerics each lane also keeps the largest |x| of its samples, and the rows are
+// checked against the conditioning guard (guard.h: sum over the channels of the measured X^2).
 template <bool FAST>
 __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* __restrict__ ep,
                                                                   int64_t n, int C, int skip,
                                                                   int nfeat, int row_stride,
-                                                                  double* __restrict__ out) {
+                                                                  double* __restrict__ out,
+                                                                  Guard guard) {
   __shared__ __attribute__((aligned(16))) double win[8 * kFeWin];
   extern __shared__ __attribute__((aligned(16))) double fsmem[];
   const int lane = threadIdx.x;
@@ -338,6 +343,7 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
     }
   };
   load(0);
+  double sx = 0.0;  // fma: sum over the channels of this lane's signal's X^2
   for (int c = 0; c < C; ++c) {
     wave_sync();  // the previous channel's LDS reads precede these writes
 #pragma unroll
@@ -352,9 +358,16 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
     const double* own = win + el * kFeWin + s * kFeSeg;
     double a6, d6;
     if constexpr (FAST) {
+      double xm = 0.0;
       dwt8_collapsed_core([&](int k) { return own[k]; },
-                          [](double v0, double v1, double& x0, double& x1) { x0 = v0; x1 = v1; },
+                          [&](double v0, double v1, double& x0, double& x1) {
+                            xm = fmax(xm, fmax(fabs(v0), fabs(v1)));
+                            x0 = v0;
+                            x1 = v1;
+                          },
                           lane & ~7, s, a6, d6);
+      xm = group8_max(xm);
+      sx += xm * xm;
     } else {
       const double* sig = win + el * kFeWin;
       double x[kIn];
@@ -368,6 +381,7 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
     }
   }
   wave_sync();
+  const double sx_row = __shfl(sx, (lane & 7) * 8, 64);  // epoch `lane`'s X^2 sum (lanes < 8)
   if (lane < ne) {
     double acc = 0.0;
     for (int i = 0; i < F; ++i) {
@@ -375,6 +389,8 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       acc = acc + f * f;  // Math.pow(f, 2) summed in index order
     }
     norm[lane] = sqrt(acc);
+    if (FAST && guard.count && guard_fails(acc, kGuardK2Collapsed, sx_row))
+      guard_flag(guard, e0 + lane);
   }
   wave_sync();
   for (int idx = lane; idx < ne * F; idx += 64) out[e0 * F + idx] = feat[idx] / norm[idx / F];
@@ -392,14 +408,20 @@ constexpr int kSmallMaxC = 16;
 #endif
 static_assert(sizeof(double) * (kSmallMaxC * kWin + kSmallMaxC * 16 + 1) <= 160 * 1024,
               "features_small_kernel's LDS exceeds one gfx950 CU");
+// Under fma numerics the row is checked against the conditioning guard (guard.h, measured X per
+// channel); a failing row is recomputed right here with the EXACT cascade from the staged windows
+// (no follow-up launch on this latency-bound path), and counted in the guard's running total.
 template <bool FAST>
 __global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
                                                              int64_t n, int C, int nfeat,
-                                                             double* __restrict__ out) {
+                                                             double* __restrict__ out,
+                                                             Guard guard) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double xs[kSmallMaxC * kWin];
   __shared__ double feat[kSmallMaxC * 16];
+  __shared__ double gx[kSmallMaxC];
   __shared__ double norm;
+  __shared__ int redo;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t e = blockIdx.x;
   const f64x2* src = (const f64x2*)(rows + e * C * kWin);
@@ -418,27 +440,55 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
   __syncthreads();
   const int F = C * nfeat;
   const int s = lane & 7;
-  for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
-    const int c = c0 + (lane >> 3);
-    const bool valid = c < C;
-    const double* xr = xs + (valid ? c : 0) * kWin;
-    double x[kIn];
+  auto bank = [&](auto fast_tag) {
+    constexpr bool FA = decltype(fast_tag)::value;
+    for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
+      const int c = c0 + (lane >> 3);
+      const bool valid = c < C;
+      const double* xr = xs + (valid ? c : 0) * kWin;
+      double x[kIn];
 #pragma unroll
-    for (int k = 0; k < kIn; ++k) x[k] = xr[(kSegLen * s + k) & (kWin - 1)];
-    double a6, d6;
-    dwt8_cascade<FAST, true>(x, nullptr, lane & ~7, s, a6, d6);
-    if (valid) {
-      if (s < nfeat) feat[c * nfeat + s] = a6;
-      if (8 + s < nfeat) feat[c * nfeat + 8 + s] = d6;
+      for (int k = 0; k < kIn; ++k) x[k] = xr[(kSegLen * s + k) & (kWin - 1)];
+      double a6, d6;
+      dwt8_cascade<FA, true>(x, nullptr, lane & ~7, s, a6, d6);
+      if constexpr (FA) {  // the guard's X: max |x| over the lane's own 64 samples, then the group
+        double xm = 0.0;
+#pragma unroll
+        for (int k = 0; k < kSegLen; ++k) xm = fmax(xm, fabs(x[k]));
+        xm = group8_max(xm);
+        if (valid && s == 0) gx[c] = xm * xm;
+      }
+      if (valid) {
+        if (s < nfeat) feat[c * nfeat + s] = a6;
+        if (8 + s < nfeat) feat[c * nfeat + 8 + s] = d6;
+      }
     }
-  }
-  __syncthreads();
+    __syncthreads();
+  };
+  if constexpr (FAST) bank(std::true_type{});
+  else bank(std::false_type{});
   if (tid == 0) {  // SignalProcessing.normalize: Math.pow(f, 2) summed in index order
     double acc = 0.0;
     for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
     norm = sqrt(acc);
+    redo = 0;
+    if (FAST && guard.total) {
+      double sx = 0.0;
+      for (int c = 0; c < C; ++c) sx += gx[c];
+      redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
+    }
   }
   __syncthreads();
+  if (FAST && redo) {  // uniform: the EXACT filter bank and normalisation on the staged windows
+    bank(std::false_type{});
+    if (tid == 0) {
+      double acc = 0.0;
+      for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
+      norm = sqrt(acc);
+      atomicAdd(guard.total, 1ull);
+    }
+    __syncthreads();
+  }
   for (int i = tid; i < F; i += 256) out[e * F + i] = feat[i] / norm;
 }
 
@@ -500,9 +550,9 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
   const bool aligned = ((uintptr_t)out & 15) == 0;  // the write pass stores 16-byte pairs
   if (!aligned) scratch = nullptr;
   if (scratch && fmt == 0 && ct == 3 && C == 3)
-    be = launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch, err);
+    be = launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch, err, nullptr);
   else if (scratch && baseline_any_supported(fmt, ct, C))
-    be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err);
+    be = launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err, nullptr);
   if (be == hipSuccess) {
     const bool small = C * (dev::kPost / 2) <= 256 * dev::kCutPairs;
     const int fbytes = ct * (fmt == 0 ? 2 : 4);
@@ -554,31 +604,37 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
 }
 
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
-                                       int nfeat, bool fast, double* out, int row_stride) {
+                                       int nfeat, bool fast, double* out, int row_stride,
+                                       const Guard& guard) {
   if (n == 0) return hipSuccess;
   const size_t smem = sizeof(double) * (8 * (size_t)C * nfeat + 8);
   dim3 grid((unsigned)((n + 7) / 8)), block(64);
-  if (fast)
+  if (fast) {
+    if (guard.count) {
+      const hipError_t e = hipMemsetAsync(guard.count, 0, sizeof(int), st);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, row_stride, out);
-  else
+                       skip, nfeat, row_stride, out, guard);
+  } else {
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<false>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, row_stride, out);
+                       skip, nfeat, row_stride, out, Guard{nullptr, nullptr, nullptr});
+  }
   return hipGetLastError();
 }
 
 bool features_small_supported(int C) { return C >= 1 && C <= dev::kSmallMaxC; }
 
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
-                                 bool fast, double* out) {
+                                 bool fast, double* out, const Guard& guard) {
   if (n == 0) return hipSuccess;
   if (!features_small_supported(C)) return hipErrorNotSupported;
   if (fast)
     hipLaunchKernelGGL(dev::features_small_kernel<true>, dim3((unsigned)n), dim3(256), 0, st, rows,
-                       n, C, nfeat, out);
+                       n, C, nfeat, out, guard);
   else
     hipLaunchKernelGGL(dev::features_small_kernel<false>, dim3((unsigned)n), dim3(256), 0, st, rows,
-                       n, C, nfeat, out);
+                       n, C, nfeat, out, Guard{nullptr, nullptr, nullptr});
   return hipGetLastError();
 }
 

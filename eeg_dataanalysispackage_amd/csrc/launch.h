@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "guard.h"
+
 namespace eegfx {
 
 constexpr int kMaxChannels = 64;
@@ -24,13 +26,17 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
                              double* out, void* scratch, int* err);
 // row_stride: doubles between consecutive (epoch, channel) rows of `ep` (750 for materialised
 // epochs, 512 for the window-only rows the host path stages)
+// guard (fma numerics): the conditioning guard's list (guard.h); its count is zeroed here and the
+// caller launches launch_guard_fixup_epochs after this kernel.
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
-                                       int nfeat, bool fast, double* out, int row_stride = 750);
+                                       int nfeat, bool fast, double* out, int row_stride,
+                                       const Guard& guard);
 // Small host batches (kernels.hip features_small_kernel): rows = n x C x 512 packed window rows,
 // one workgroup per epoch, C <= 16; rows / out may be device pointers of mapped pinned memory.
 bool features_small_supported(int C);
+// guard.total counts the rows the kernel recomputed under EXACT (guard.h); count/list unused.
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
-                                 bool fast, double* out);
+                                 bool fast, double* out, const Guard& guard);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
 // Non-temporal reads pay when the regions neighbouring epochs read do not overlap: the average
@@ -43,12 +49,14 @@ bool streaming_reads(int64_t n_frames, int64_t n, int64_t min_spacing);
 // the rest.
 bool fused_supported(int fmt, int ct, int C, const double* out);
 size_t fused_scratch_bytes(int64_t n, int C);
+// guard_count: zeroed by the baseline kernel (nullptr: no guard); the window kernel appends the
+// rows that fail the conditioning guard (fma) and the caller launches launch_guard_fixup_raw.
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 void* scratch, int* err);
+                                 void* scratch, int* err, int* guard_count);
 hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                               const void* scratch, double* out);
+                               const void* scratch, double* out, const Guard& guard);
 // Algorithmic HBM bytes per epoch of window_kernel (the dominant kernel): window frames, the
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);
@@ -60,10 +68,18 @@ bool wide_supported(int fmt, int ct, int C);
 bool baseline_any_supported(int fmt, int ct, int C);
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch, int* err);
+                               void* scratch, int* err, int* guard_count);
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                              const void* scratch, double* out);
+                              const void* scratch, double* out, const Guard& guard);
+
+// guard.hip: the EXACT recomputation of the rows a guarded launch flagged (no-op when
+// g.count is null).  raw: the same recording / positions / baselines (scratch) as the fused launch.
+hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int64_t n_frames,
+                                  int ct, const ChanSel& sel, int C, const int64_t* pos,
+                                  const void* scratch, const Guard& g, double* out);
+hipError_t launch_guard_fixup_epochs(hipStream_t st, const double* ep, int C, int skip, int nfeat,
+                                     int row_stride, const Guard& g, double* out);
 
 // logreg.hip: MLlib LogisticRegressionWithSGD (full batch) on device.  State block: iteration
 // count, flag (0 running, 1 converged / done, 2 invalid labels), then the d weights.

@@ -20,6 +20,7 @@
 #include <cstdint>
 
 #include "dwt8.h"
+#include "guard.h"
 #include "launch.h"
 #include "lds_dma.h"
 
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
                                                            int C, const int64_t* __restrict__ pos,
                                                            int64_t n, int EB, int BSTQ,
                                                            float* __restrict__ bout,
-                                                           int* __restrict__ err) {
+                                                           int* __restrict__ err,
+                                                           int* __restrict__ guard_count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t sB[256];
   const int FB = ct * (int)sizeof(T);
@@ -50,6 +52,8 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = blockDim.x / 64;
   const int NQ = BSTQ - 1;  // quads staged per epoch
+  // the window kernel that follows appends to the guard list (fma numerics)
+  if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
   const int rows = (NQ + 63) / 64;
   if (tid < ne) {
     const int64_t p = pos[e0 + tid];
@@ -131,14 +135,15 @@ __device__ __forceinline__ float sample_at(const uint8_t* p) {
 }
 
 // Per-workgroup LDS: EPW epochs x 8 segment blocks of SEGQ quads, then EPW x F features, then
-// EPW norms.  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame; FBC != 0 fixes FB at compile
+// EPW norms, then (fma) the guard's EPW x C per-signal X^2 (guard.h: int16 from r and b, float32
+// the measured max |x|).  SEGQ = 4*FB + 1, FB = ct*sizeof(T) bytes per frame; FBC != 0 fixes FB at compile
 // time (configs[3]'s 32-channel int16 montage: 64), so every sample read of the decode is an
 // immediate LDS offset instead of an address computed per sample.
 template <typename T, bool FAST, int EPW, int FBC = 0, bool STREAM = false>
 __global__ __launch_bounds__(256) void window_wide_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
     const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
-    double* __restrict__ out) {
+    double* __restrict__ out, Guard guard) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int FB = FBC ? FBC : ct * (int)sizeof(T);
   const int SEGQ = 4 * FB + 1;
@@ -147,6 +152,7 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
   uint8_t* win = smem;
   double* feat = (double*)(smem + (size_t)EPW * EQ * 16);
   double* norm = feat + EPW * F;
+  double* gx = norm + EPW;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * EPW;
   const int ne = (n - e0) < EPW ? (int)(n - e0) : EPW;
@@ -208,13 +214,18 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     const float b = valid ? base[(e0 + m) * C + c] : 0.0f;
     double a6, d6;
     if constexpr (FAST) {  // the 8 lanes of a group share the signal: partial-sum halos
-#if EEGFX_COLLAPSED
-      dwt8_collapsed_cascade([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
-                             a6, d6);
-#else
-      dwt8_fast_cascade([&](int k) { return sample_at<T>(own + k * FB); }, r, b, lane & ~7, s,
-                        a6, d6);
-#endif
+      constexpr bool MEASURE = !std::is_same<T, int16_t>::value;  // no a-priori bound for float32
+      float ym = 0.0f;
+      dwt8_collapsed_cascade<MEASURE>([&](int k) { return sample_at<T>(own + k * FB); }, r, b,
+                                      lane & ~7, s, a6, d6, &ym);
+      double x2;
+      if constexpr (MEASURE) {
+        const double X = (double)group8_max(ym);
+        x2 = X * X;
+      } else {
+        x2 = guard_x2_int16(r, b);
+      }
+      if (valid && s == 0) gx[m * C + c] = x2;
     } else {
       double a1[40];
       (void)nxt;
@@ -235,8 +246,15 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
     for (int m = w; m < ne; m += blockDim.x / 64) {
       double acc = 0.0;
       for (int i = lane; i < F; i += 64) acc = __builtin_fma(feat[m * F + i], feat[m * F + i], acc);
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) norm[m] = rsqrt_nr(acc);  // the reciprocal norm (multiplied below)
+      double sx = lane < C ? gx[m * C + lane] : 0.0;  // C <= 64
+      for (int off = 32; off > 0; off >>= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        sx += __shfl_xor(sx, off, 64);
+      }
+      if (lane == 0) {
+        norm[m] = rsqrt_nr(acc);  // the reciprocal norm (multiplied below)
+        if (guard.count && guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(guard, e0 + m);
+      }
     }
   } else {
     // the reference's sequential fold, index order, one lane per epoch
@@ -271,12 +289,13 @@ template <bool FAST, bool STREAM>
 __global__ __launch_bounds__(256) void window_c32_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
     const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
-    double* __restrict__ out) {
+    double* __restrict__ out, Guard guard) {
   constexpr int C = 32, FB = 64, SEGQ = 4 * FB + 1, EQ = 8 * SEGQ, F = 16 * C;
   constexpr int NROWS = (EQ + 63) / 64;  // 33
   __shared__ __attribute__((aligned(16))) uint8_t win[EQ * 16];
   __shared__ __attribute__((aligned(16))) double feat[F];
   __shared__ double norm1;
+  __shared__ double gx[FAST ? C : 1];  // the guard's X^2 per channel (fma numerics)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
   const int64_t nbytes = n_frames * FB;
@@ -343,6 +362,7 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   }
   feat[c * 16 + s] = a6;
   feat[c * 16 + 8 + s] = d6;
+  if (FAST && s == 0) gx[c] = guard_x2_int16(r, b);
   __syncthreads();
   double* o = out + e * F;
   if constexpr (FAST) {
@@ -350,9 +370,16 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
       double acc = 0.0;
 #pragma unroll
       for (int k = 0; k < F / 64; ++k) acc = __builtin_fma(feat[lane + 64 * k], feat[lane + 64 * k], acc);
+      double sx = lane < C ? gx[lane] : 0.0;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) norm1 = rsqrt_nr(acc);
+      for (int off = 32; off > 0; off >>= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        sx += __shfl_xor(sx, off, 64);
+      }
+      if (lane == 0) {
+        norm1 = rsqrt_nr(acc);
+        if (guard.count && guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(guard, e);
+      }
     }
     __syncthreads();
     const double inv = norm1;
@@ -383,12 +410,13 @@ namespace {
 template <typename T, bool FAST, int EPW, int FBC = 0, bool STREAM = false>
 hipError_t launch_wide_t(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                          const ChanSel& sel, int C, const int64_t* pos, const float* base,
-                         int64_t n, double* out) {
+                         int64_t n, double* out, const Guard& guard) {
   const int FB = ct * (int)sizeof(T);
-  const size_t lds = (size_t)EPW * 8 * (4 * FB + 1) * 16 + (size_t)EPW * 16 * C * 8 + EPW * 8;
+  const size_t lds = (size_t)EPW * 8 * (4 * FB + 1) * 16 + (size_t)EPW * 16 * C * 8 + EPW * 8 +
+                     (FAST ? (size_t)EPW * C * 8 : 0);
   const dim3 grid((unsigned)((n + EPW - 1) / EPW));
   hipLaunchKernelGGL((dev::window_wide_kernel<T, FAST, EPW, FBC, STREAM>), grid, dim3(256), lds, st,
-                     (const uint8_t*)raw, n_frames, ct, sel, C, pos, base, n, out);
+                     (const uint8_t*)raw, n_frames, ct, sel, C, pos, base, n, out, guard);
   return hipGetLastError();
 }
 }  // namespace
@@ -397,7 +425,7 @@ hipError_t launch_wide_t(hipStream_t st, const void* raw, int64_t n_frames, int 
 // while that fits comfortably (two or more workgroups per CU), one otherwise.
 static size_t wide_lds_per_epoch(int fmt, int ct, int C) {
   const int FB = ct * (fmt == 0 ? 2 : 4);
-  return (size_t)8 * (4 * FB + 1) * 16 + (size_t)16 * C * 8 + 8;
+  return (size_t)8 * (4 * FB + 1) * 16 + (size_t)16 * C * 8 + 8 + (size_t)C * 8;
 }
 
 bool wide_supported(int fmt, int ct, int C) {
@@ -423,7 +451,7 @@ bool baseline_any_supported(int fmt, int ct, int C) {
 
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch, int* err) {
+                               void* scratch, int* err, int* guard_count) {
   if (n == 0) return hipSuccess;
   int BSTQ = 0;
   const int EB = baseline_any_tile(fmt, ct, C, &BSTQ);
@@ -431,31 +459,34 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
   const dim3 grid((unsigned)((n + EB - 1) / EB));
   if (fmt == 0 && streaming_reads(n_frames, n, dev::kPre + 687))  // pre-stimulus frames unshared
     hipLaunchKernelGGL((dev::baseline_any_kernel<int16_t, true>), grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
+                       guard_count);
   else if (fmt == 0)
     hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
+                       guard_count);
   else
     hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), lds, st,
-                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err);
+                       (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
+                       guard_count);
   return hipGetLastError();
 }
 
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                              const void* scratch, double* out) {
+                              const void* scratch, double* out, const Guard& guard) {
   if (n == 0) return hipSuccess;
   const float* base = (const float*)scratch;
   const bool two = wide_lds_per_epoch(fmt, ct, C) <= 32 * 1024;  // dynamic LDS stays <= 64 KB
 #define EEGFX_W(T, FA)                                                                        \
-  return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out)       \
-             : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
+  return two ? launch_wide_t<T, FA, 2>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard)       \
+             : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard);
   if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) {  // configs[3]
     const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
     const dim3 g((unsigned)n);
 #define EEGFX_C32(FA, NTV) \
     hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV>), g, dim3(256), 0, st, (const uint8_t*)raw, \
-                       n_frames, sel, pos, base, n, out)
+                       n_frames, sel, pos, base, n, out, guard)
     if (fast) { if (nt) EEGFX_C32(true, true); else EEGFX_C32(true, false); }
     else { if (nt) EEGFX_C32(false, true); else EEGFX_C32(false, false); }
 #undef EEGFX_C32
@@ -464,10 +495,10 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
   if (fmt == 0 && ct == 32 && !two) {  // the frame size as a compile-time constant
     // streaming (non-temporal) window reads and row stores when the windows are disjoint
     if (streaming_reads(n_frames, n, dev::kWin + 8))
-      return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
-                  : launch_wide_t<int16_t, false, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
-    return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out)
-                : launch_wide_t<int16_t, false, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out);
+      return fast ? launch_wide_t<int16_t, true, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard)
+                  : launch_wide_t<int16_t, false, 1, 64, true>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard);
+    return fast ? launch_wide_t<int16_t, true, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard)
+                : launch_wide_t<int16_t, false, 1, 64>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard);
   }
   if (fmt == 0) {
     if (fast) { EEGFX_W(int16_t, true) } else { EEGFX_W(int16_t, false) }

@@ -24,10 +24,20 @@
  * synchronising -- call eegfx_ctx_synchronize()).  Device-resident marker positions are
  * validated by the kernels that read them (OffLineDataProvider.java:220-225: pos-100 must lie
  * in [0, n_frames]); a violation is reported as EEGFX_ERANGE by the next call on that context
- * that synchronises it -- eegfx_ctx_synchronize, or any EEGFX_MEM_HOST compute call -- which
- * also clears it.  Results of EEGFX_MEM_DEVICE calls are unspecified until such a call has
- * returned EEGFX_OK.  Host positions are checked before any work is enqueued and fail the call
- * itself.
+ * that synchronises it, which also clears it.  The calls that synchronise are
+ * eegfx_ctx_synchronize, eegfx_ctx_guard_stats, every EEGFX_MEM_HOST compute call,
+ * eegfx_read_raw with EEGFX_MEM_DEVICE, eegfx_logreg_sgd_train / eegfx_svm_sgd_train, and
+ * eegfx_logreg_predict / eegfx_svm_predict with EEGFX_MEM_DEVICE.  When such a call returns
+ * EEGFX_ERANGE for an earlier call's position, its own work has completed and its outputs are
+ * valid; the rows of the epochs with the refused positions are unspecified.  Results of
+ * EEGFX_MEM_DEVICE calls are unspecified until a synchronising call has returned EEGFX_OK.  Host
+ * positions are checked before any work is enqueued and fail the call itself.
+ *
+ * Numerics: EEGFX_EXACT reproduces the reference's fp64 operation order value for value;
+ * EEGFX_FMA runs the fused-multiply-add filter bank and is within 1e-9 of it on every row: a
+ * conditioning guard bounds each row's rounding difference from the EXACT row,
+ * and the rows it cannot certify (features at rounding level, e.g. a window in the filters' null
+ * space) are recomputed under EXACT on the device before the call's results are complete.
  */
 #ifndef EEGFX_H_
 #define EEGFX_H_
@@ -68,7 +78,8 @@ extern "C" {
 
 /* numerics of the DWT filter bank */
 #define EEGFX_EXACT 0   /* separate fp64 mul + add in the reference order: bit-exact to Java */
-#define EEGFX_FMA 1     /* fp64 fused multiply-add: within 1e-9 relative, fewer instructions  */
+#define EEGFX_FMA 1     /* fp64 fused multiply-add: within 1e-9 relative, fewer instructions;
+                           rows the conditioning guard cannot certify are recomputed EXACT */
 
 typedef struct eegfx_ctx eegfx_ctx;
 typedef struct eegfx_odp eegfx_odp;
@@ -98,6 +109,11 @@ int eegfx_ctx_synchronize(eegfx_ctx* ctx);
 int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable);
 int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,
                            int64_t* total_bytes);
+/* The fma numerics' conditioning guard: rows that went through a guarded (EEGFX_FMA) feature
+ * launch on this context, and rows the guard recomputed under EEGFX_EXACT, since the context was
+ * created or last reset (reset != 0 clears both after reading).  Synchronises the context. */
+int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_recomputed,
+                          int reset);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
 /* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */
