@@ -93,8 +93,13 @@ def parse():
                          "(reported under 'alt_numerics'; 0 disables)")
     ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="epochs in the CPU-baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: every available host core (affinity, capped by a cgroup CPU quota)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL feature gather legs")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed steps after the warmup for at least this much wall time, so the "
+                         "timed steps start past the clock's power-cap transient (reported as "
+                         "config.settle; DESIGN.md §7); 0 disables")
     ap.add_argument("--trace-steps", action="store_true",
                     help="study only: device time of every warmup and timed step (HIP events "
                          "between steps), reported under 'step_trace'")
@@ -267,6 +272,7 @@ def main():
         ctx.process_recording(raw, ct, cols, res, pos, out=out)
 
     trace = {"warmup": [], "timed": []} if args.trace_steps else None
+    ctx.guard_stats(reset=True)
 
     def traced(k, key):
         if trace is None:
@@ -282,6 +288,16 @@ def main():
 
     traced(args.warmup, "warmup")
     torch.cuda.synchronize(dev)
+    # Settle: the first ~25 launches after idle run at a clock that first overshoots, then sinks
+    # below and recovers to the power-capped steady state (step trace, profiles/r04c/driver_gap);
+    # a short --warmup would otherwise time that transient.  Reported, not counted as warmup.
+    settle_steps, s0 = 0, time.perf_counter()
+    while (time.perf_counter() - s0) * 1e3 < args.settle_ms:
+        for _ in range(10):
+            step()
+        settle_steps += 10
+        torch.cuda.synchronize(dev)
+    settle_ms = (time.perf_counter() - s0) * 1e3
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -305,6 +321,7 @@ def main():
         raise RuntimeError(f"timed {launches} window_kernel launches for {args.steps} steps")
     kernel_ms = win_total_ms / launches                 # average window_kernel launch duration
     kernel_bytes = win_bytes // launches                # algorithmic bytes per launch
+    guard_checked, guard_redone = ctx.guard_stats()     # warmup + timed steps (fma numerics)
 
     t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64, device=dev)
     if distributed:
@@ -369,6 +386,12 @@ def main():
                 "numerics": args.numerics,
                 "kernels": kernels,
                 "unit_rows_check": ok_norm,
+                "guard": guard_report(args, fx, dev, guard_checked, guard_redone),
+                "settle": {"min_ms": args.settle_ms, "ms": round(settle_ms, 1),
+                           "steps": settle_steps,
+                           "note": "untimed steps between the warmup and the timed region, until "
+                                   "min_ms of wall time has passed (the power-cap clock "
+                                   "transient of the first ~25 launches)"},
             },
             "roofline": {
                 "bound": "hbm",
@@ -441,6 +464,32 @@ def main():
     if distributed:
         dist.destroy_process_group()
     watchdog.disarm()
+
+
+def guard_report(args, fx, dev, checked, redone):
+    """The fma conditioning guard: rows of the timed run it could not certify and
+    sent to the EXACT follow-up launch, and the same rate on every marker of the reference's two
+    recordings (tests/golden/test-data, the repo's copies), outside the timed region."""
+    if args.numerics != "fma":
+        return None
+    rep = {"rows_checked": checked, "rows_recomputed": redone,
+           "rate": (redone / checked) if checked else None, "reference_recordings": {}}
+    data = os.path.join(REPO, "tests", "golden", "test-data", "DoD")
+    c = fx.Context(dev.index, numerics="fma")
+    try:
+        for stem in ("DoD2015_01", "DoD_2015_02"):
+            base = os.path.join(data, stem)
+            raw = fx.read_raw(base + ".vhdr", base + ".eeg")
+            allpos = [m.position for m in fx.read_markers(base + ".vmrk") if m.position >= 100]
+            c.guard_stats(reset=True)
+            c.process_recording(raw, raw.shape[1], [0, 1, 2], [0.1] * 3, allpos)
+            k, r = c.guard_stats()
+            rep["reference_recordings"][stem] = {"markers": k, "rows_recomputed": r}
+    except Exception as exc:  # the recordings are test fixtures; report, do not fail the line
+        rep["reference_recordings"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
+    finally:
+        c.close()
+    return rep
 
 
 class _Watchdog:
@@ -829,6 +878,29 @@ def bench_logreg(args, rank, world, dev, dist):
     ctx.close()
 
 
+def host_cores():
+    """The host cores this process may run on: the CPU affinity set, capped by a cgroup CPU quota
+    when one is set (a GPU box shares its host: nproc shows every CPU of the machine, the quota
+    the box's share).  Returns (cores, details)."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    cores = min(aff, max(1, math.floor(quota))) if quota else aff
+    return cores, {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
     """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
     threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload.
@@ -838,7 +910,10 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
     the features, 4 epochs per AVX2 vector, bit-identical features), and both at one thread on a
     smaller sample.  Every leg is the median of 5 timed runs after a warm-up."""
     from oracle import oracle
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    avail, cores_info = host_cores()
+    # SURVEY 8d / BASELINE.md: N = every core of the host available to this run (Spark local[*],
+    # Utils/SparkInitializer.java:44); --cpu-threads overrides
+    threads = args.cpu_threads or avail
     k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10, args.epochs)
     k1 = max(1, min(k // 25, 20000 if C == 3 else 2000))  # one-thread sample
     host = raw[: sp * k + 2000].cpu().numpy()
@@ -871,10 +946,14 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
     faithful_1, _, _ = leg(k1, True, 1)
     minimal_n, _, feats_min = leg(k, False, threads)
     minimal_1, _, _ = leg(k1, False, 1)
+    t16 = None
+    if threads != 16 and avail >= 16:  # the earlier rounds' 16-thread leg, for comparison
+        t16 = {"value": round(leg(k, True, 16)[0], 1), "cores": 16, "sample_epochs": k}
     return {
         "value": round(value, 1),
         "unit": "epochs/s",
         "cores": threads,
+        "host_cores": cores_info,
         "kind": "port",
         "sample": f"first {k} epochs of the rank-0 synthetic recording, C restatement of the "
                   f"Java path (full 6-level pyramid), {threads} threads over contiguous ranges, "
@@ -886,6 +965,7 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
                                 "bit_identical_to_faithful": bool(np.array_equal(
                                     feats, feats_min, equal_nan=True))},
             "optimised_1_thread": {"value": round(minimal_1, 1), "sample_epochs": k1},
+            "faithful_16_threads": t16,
         },
     }
 

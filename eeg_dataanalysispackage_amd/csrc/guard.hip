@@ -21,6 +21,15 @@
 #include "launch.h"
 
 namespace eegfx {
+
+// The follow-up launch: kGuardGrid workgroups of kGuardBlock threads loop over the flagged rows
+// (one row per workgroup at a time, 8 lanes per signal).  Small, because it runs after every
+// guarded launch and nearly always finds the list empty: 128 x 256 measured 4.8 us per launch
+// (2.7 us minimum) on the bench step (profiles/r04c); an input that flags many rows is still
+// recomputed correctly, at 16 rows at a time.
+constexpr int kGuardGrid = 16;
+constexpr int kGuardBlock = 128;
+
 namespace dev {
 
 // Window samples of (epoch e, channel c) from the multiplexed recording: frame pos + 175 + k.
@@ -67,18 +76,19 @@ struct EpochWindows {
 };
 
 template <typename Src>
-__global__ __launch_bounds__(256) void exact_rows_kernel(Src src, int nfeat, Guard g,
-                                                         double* __restrict__ out) {
+__global__ __launch_bounds__(kGuardBlock) void exact_rows_kernel(Src src, int nfeat, Guard g,
+                                                                 double* __restrict__ out) {
   __shared__ double feat[kMaxChannels * 16];
   __shared__ double norm;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, s = lane & 7;
+  constexpr int SIG = kGuardBlock / 8;  // signals per pass
   const int cnt = *g.count;  // written by the guarded kernel before this launch
   if (blockIdx.x == 0 && tid == 0 && cnt > 0) atomicAdd(g.total, (unsigned long long)cnt);
   const int C = src.C;
   const int F = C * nfeat;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {  // uniform
     const int64_t e = g.list[i];
-    for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
+    for (int c0 = 8 * w; c0 < C; c0 += SIG) {  // uniform per wave
       const int c = c0 + (lane >> 3);
       const bool valid = c < C;
       double x[kIn];
@@ -97,16 +107,12 @@ __global__ __launch_bounds__(256) void exact_rows_kernel(Src src, int nfeat, Gua
       norm = sqrt(acc);
     }
     __syncthreads();
-    for (int k = tid; k < F; k += 256) out[e * F + k] = feat[k] / norm;
+    for (int k = tid; k < F; k += kGuardBlock) out[e * F + k] = feat[k] / norm;
     __syncthreads();
   }
 }
 
 }  // namespace dev
-
-// Workgroups of the follow-up launch: enough to recompute many rows at once if an input flags
-// them (an adversarial recording), few enough that an empty list costs one short launch.
-constexpr int kGuardGrid = 128;
 
 hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int64_t n_frames,
                                   int ct, const ChanSel& sel, int C, const int64_t* pos,
@@ -116,12 +122,12 @@ hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int6
     dev::RawWindows<int16_t> src{(const uint8_t*)raw, n_frames, ct, sel, pos,
                                  (const float*)scratch, C};
     hipLaunchKernelGGL(dev::exact_rows_kernel<dev::RawWindows<int16_t>>, dim3(kGuardGrid),
-                       dim3(256), 0, st, src, 16, g, out);
+                       dim3(kGuardBlock), 0, st, src, 16, g, out);
   } else {
     dev::RawWindows<float> src{(const uint8_t*)raw, n_frames, ct, sel, pos, (const float*)scratch,
                                C};
-    hipLaunchKernelGGL(dev::exact_rows_kernel<dev::RawWindows<float>>, dim3(kGuardGrid), dim3(256),
-                       0, st, src, 16, g, out);
+    hipLaunchKernelGGL(dev::exact_rows_kernel<dev::RawWindows<float>>, dim3(kGuardGrid),
+                       dim3(kGuardBlock), 0, st, src, 16, g, out);
   }
   return hipGetLastError();
 }
@@ -130,7 +136,7 @@ hipError_t launch_guard_fixup_epochs(hipStream_t st, const double* ep, int C, in
                                      int row_stride, const Guard& g, double* out) {
   if (!g.count) return hipSuccess;
   dev::EpochWindows src{ep, row_stride, skip, C};
-  hipLaunchKernelGGL(dev::exact_rows_kernel<dev::EpochWindows>, dim3(kGuardGrid), dim3(256), 0,
+  hipLaunchKernelGGL(dev::exact_rows_kernel<dev::EpochWindows>, dim3(kGuardGrid), dim3(kGuardBlock), 0,
                      st, src, nfeat, g, out);
   return hipGetLastError();
 }
