@@ -304,19 +304,18 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
                            const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                            double* out) {
   const bool fast = ctx->numerics != EEGFX_EXACT;
-  // fma: rows that fail the conditioning guard are recomputed under EXACT by a follow-up launch
-  // (guard.h, guard.hip); the baseline kernel zeroes the guard count
+  // fma: rows that fail the conditioning guard (guard.h) are recomputed under EXACT -- inside the
+  // kernel that flags them, or (the generic any-layout kernels) by a follow-up launch over the
+  // guard list that launch_window_wide issues; baseline_any_kernel zeroes the list's count
   const Guard g = ctx->guard_for(n);
   if (fused_supported(fmt, ct, C, out)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch,
-                                    ctx->err_dev, g.count));
+                                    ctx->err_dev, nullptr));
     ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
     HIP_CHECK(launch_fused_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fast, fscratch,
                                   out, g));
     ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
-    HIP_CHECK(launch_guard_fixup_raw(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, fscratch, g,
-                                     out));
     return;
   }
   if (wide_supported(fmt, ct, C)) {
@@ -328,8 +327,6 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
                                  fscratch, out, g));
     const int64_t elem = fmt == EEGFX_INT_16 ? 2 : 4;
     ctx->toc(n * (EEGFX_DWT8_EPOCH_SIZE * ct * elem + C * 4 + 8 + C * 16 * 8));
-    HIP_CHECK(launch_guard_fixup_raw(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, fscratch, g,
-                                     out));
     return;
   }
   double* ep = (double*)ctx->scratch.get(sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS);
@@ -339,8 +336,6 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   HIP_CHECK(launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
                                         EEGFX_DWT8_FEATURE_SIZE, fast, out, EEGFX_POSTSTIMULUS, g));
   ctx->toc(0);
-  HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, ep, C, EEGFX_DWT8_SKIP, EEGFX_DWT8_FEATURE_SIZE,
-                                      EEGFX_POSTSTIMULUS, g, out));
 }
 
 }  // namespace
@@ -813,8 +808,6 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)dwin, m, C, 0,
                                               feature_size, ctx->numerics != EEGFX_EXACT, rows,
                                               EEGFX_DWT8_EPOCH_SIZE, g));
-        HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, (const double*)dwin, C, 0, feature_size,
-                                            EEGFX_DWT8_EPOCH_SIZE, g, rows));
       }
       ctx->toc(0);
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -829,8 +822,6 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
                                           ctx->numerics != EEGFX_EXACT, d_out, EEGFX_POSTSTIMULUS,
                                           g));
     ctx->toc(0);
-    HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, d_in, C, skip, feature_size,
-                                        EEGFX_POSTSTIMULUS, g, d_out));
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
       ctx->drain();
@@ -1250,8 +1241,6 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
                                           odp->n_epochs, 3, skip, feature_size,
                                           ctx->numerics != EEGFX_EXACT, d_out, EEGFX_POSTSTIMULUS,
                                           g));
-    HIP_CHECK(launch_guard_fixup_epochs(ctx->stream, (const double*)odp->d_epochs, 3, skip,
-                                        feature_size, EEGFX_POSTSTIMULUS, g, d_out));
     HIP_CHECK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     ctx->drain();
   });

@@ -518,6 +518,71 @@ __device__ __forceinline__ double rsqrt_nr(double v) {
   return r;
 }
 
+// One feature row under EXACT numerics by one wave, for the rare rows the fma numerics'
+// conditioning guard cannot certify (guard.h): for each of the C channels the 512 window samples
+// (sample(c, k): the decoded doubles) go to LDS, the six levels run with every output
+// sum_j x[(2i + j) mod n] h[j] (g[j] at level 6) in the reference's order -- one rounded multiply
+// and one rounded add per tap, the file compiled with -ffp-contract=off -- so the row equals the
+// EXACT kernels' value for value; then SignalProcessing.normalize (sequential sum of squares, sqrt,
+// divide).  row: C * nfeat doubles of LDS (receives the normalised row); scratch: 768 doubles of
+// LDS that no other wave touches.  Few registers: it runs inside the fma kernels' rare path.
+static __constant__ double kHG[2 * kTaps] = {
+    EEGFX_H0, EEGFX_H1, EEGFX_H2, EEGFX_H3, EEGFX_H4, EEGFX_H5, EEGFX_H6, EEGFX_H7, EEGFX_H8,
+    EEGFX_H9, tap_g(0), tap_g(1), tap_g(2), tap_g(3), tap_g(4), tap_g(5), tap_g(6), tap_g(7),
+    tap_g(8), tap_g(9)};
+template <typename Sample>
+__device__ __forceinline__ void dwt8_exact_row_wave(Sample sample, int C, int nfeat,
+                                                    double* scratch, double* row, int lane) {
+  // loops kept rolled and the taps read from kHG: the kernels this is inlined into keep their
+  // register budget (the unrolled form raised the 3-channel window kernel from 44 to 94 VGPRs)
+#pragma unroll 1
+  for (int c = 0; c < C; ++c) {
+    double* in = scratch;
+    double* out = scratch + kWin;
+#pragma unroll 1
+    for (int k = lane; k < kWin; k += 64) in[k] = sample(c, k);
+    wave_sync();
+    int n = kWin;
+#pragma unroll 1
+    for (int level = 1; level <= 5; ++level) {
+#pragma unroll 1
+      for (int i = lane; i < n / 2; i += 64) {
+        double a = in[2 * i] * kHG[0];
+#pragma unroll 1
+        for (int j = 1; j < kTaps; ++j) a = a + in[(2 * i + j) & (n - 1)] * kHG[j];
+        out[i] = a;
+      }
+      wave_sync();
+      double* t = in;
+      in = out;
+      out = t;
+      n /= 2;
+    }
+    if (lane < 16) {  // level 6 on the 16 values of a5: a6[i] (lanes 0-7), d6[i] (lanes 8-15)
+      const int i = lane & 7;
+      const double* f = kHG + (lane >= 8 ? kTaps : 0);
+      double a = in[2 * i] * f[0];
+#pragma unroll 1
+      for (int j = 1; j < kTaps; ++j) a = a + in[(2 * i + j) & 15] * f[j];
+      const int k = lane >= 8 ? 8 + i : i;
+      if (k < nfeat) row[c * nfeat + k] = a;
+    }
+    wave_sync();
+  }
+  const int F = C * nfeat;
+  if (lane == 0) {
+    double acc = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < F; ++k) acc = acc + row[k] * row[k];
+    scratch[0] = sqrt(acc);
+  }
+  wave_sync();
+  const double nv = scratch[0];
+#pragma unroll 1
+  for (int k = lane; k < F; k += 64) row[k] = row[k] / nv;
+  wave_sync();
+}
+
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).
 // xch: this wave's exchange area (64 lanes * kSlot doubles); gbase = first lane of the group.
 // Returns a6[s] and d6[s].

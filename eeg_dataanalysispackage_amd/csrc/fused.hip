@@ -150,7 +150,7 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   const int64_t nbytes = n_frames * G::FB;
   const int64_t t0 = (int64_t)blockIdx.x * TILE;
   const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
-  // the window kernel that follows appends to the guard list (fma numerics)
+  // a window kernel that follows may append to the guard list (fma numerics)
   if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
   if (tid < TILE) {
     const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
@@ -237,12 +237,16 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
 //          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
 //          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).  A row
 //          whose sum of squares fails the conditioning guard (guard.h; gx = the C per-signal X^2)
-//          is appended to the guard list for the EXACT follow-up launch.
-template <int F, bool FAST, int C = F / 16>
+//          is recomputed under EXACT by redo(e, row) into its row slot before the store (rare:
+//          never on the bench workload), and counted in the guard's running total.
+struct NoRedo {
+  __device__ void operator()(int, double*) const {}
+};
+template <int F, bool FAST, int C = F / 16, typename Redo = NoRedo>
 __device__ __forceinline__ void normalise_store(double* fb, double* norm, double* o, int ne,
                                                 int lane, const double* gx = nullptr,
                                                 Guard g = Guard{nullptr, nullptr, nullptr},
-                                                int64_t e0 = 0) {
+                                                Redo redo = Redo{}) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   if constexpr (FAST) {
     static_assert(F % 16 == 0, "8 lanes per row, pairs of features");
@@ -258,11 +262,12 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
-    if (g.count && p == 0 && e < ne) {
+    bool fails = false;
+    if (g.total && p == 0 && e < ne) {
       double sx = 0.0;
 #pragma unroll
       for (int c = 0; c < C; ++c) sx += gx[e * C + c];
-      if (guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(g, e0 + e);
+      fails = guard_fails(acc, kGuardK2Collapsed, sx);
     }
     const double inv = rsqrt_nr(acc);
     if (e < ne) {
@@ -271,6 +276,15 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
         *(double2*)(fb + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
     }
     wave_sync();
+    uint64_t flagged = __ballot(fails);  // bit 8e: row e failed the guard
+    if (flagged) {                        // uniform, rare
+      if (lane == 0) atomicAdd(g.total, (unsigned long long)__popcll(flagged));
+      do {
+        const int e1 = __ffsll((unsigned long long)flagged) - 1;
+        redo(e1 >> 3, fb + (e1 >> 3) * F);
+        flagged &= flagged - 1;
+      } while (flagged);
+    }
     for (int i = 2 * lane; i < ne * F; i += 128)
       __builtin_nontemporal_store(*(const f64x2*)(fb + i), (f64x2*)(o + i));
     wave_sync();
@@ -437,8 +451,26 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   fb[slot] = a6;
   fb[slot + 8] = d6;
   __syncthreads();
-  if (w == 0)
-    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, e0);
+  if (w == 0) {
+    // the guard's rare path: the row recomputed under EXACT from the recording by this wave, with
+    // the LDS past the 8 feature rows as scratch (every other wave is done with the window)
+    auto redo = [&](int e, double* row) {
+      const int64_t B = wb[e0 + e] & ~(int64_t)1;  // byte offset of the window (frame pos + 175)
+      const int64_t f0 = B / G::FB;
+      dwt8_exact_row_wave(
+          [&](int c, int k) {
+            const float rc = sel.res[c], bc = base[(e0 + e) * C + c];
+            const float v = f0 + k < n_frames
+                                ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
+                                : 0.0f;
+            float y = v * rc;
+            y = y - bc;
+            return (double)y;
+          },
+          C, 16, fb + kSub * F, row, lane);
+    };
+    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo);
+  }
 }
 
 }  // namespace dev

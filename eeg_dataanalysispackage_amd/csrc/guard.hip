@@ -1,6 +1,8 @@
-// guard.hip -- the follow-up launch of the fma numerics' conditioning guard (guard.h).
+// guard.hip -- the follow-up launch of the fma numerics' conditioning guard (guard.h) for the
+// generic any-layout kernels (wide.hip window_wide_kernel; the 3- and 32-channel window kernels and
+// the batch extract recompute their flagged rows themselves, dwt8_exact_row_wave).
 //
-// The fma kernels append every row whose sum of squares fails the guard to a list; this kernel
+// The generic kernels append every row whose sum of squares fails the guard to a list; this kernel
 // recomputes exactly those rows with the EXACT filter bank (dwt8_cascade<false>: each tap one
 // rounded multiply and one rounded add in the reference's order, WaveletTransform.java:126-137)
 // and the reference's sequential normalisation (SignalProcessing.java:38-52), overwriting the fma
@@ -9,9 +11,8 @@
 // so a recomputed row is value-identical to the EXACT path's row.
 //
 // Launched right after the guarded kernel on the same stream with a fixed grid that reads the
-// device-side count: no host synchronisation, and when nothing was flagged (every row of the
-// bench workload and of the reference recordings' selected epochs) every workgroup
-// exits after one load.  Rows are few; each is read straight from memory (no LDS staging).
+// device-side count: no host synchronisation; when nothing was flagged every workgroup exits after
+// one load (~4-5 us per launch, profiles/r04d).  Rows are few; each is read straight from memory.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -59,19 +60,6 @@ struct RawWindows {
       y = y - b;
       x[k] = (double)y;
     }
-  }
-};
-
-// Window samples of caller-supplied epochs double[n][C][row_stride] from column `skip`.
-struct EpochWindows {
-  const double* ep;
-  int row_stride;
-  int skip;
-  int C;
-  __device__ __forceinline__ void window(int64_t e, int c, int s, double (&x)[kIn]) const {
-    const double* row = ep + (e * C + c) * (int64_t)row_stride + skip;
-#pragma unroll
-    for (int k = 0; k < kIn; ++k) x[k] = row[(kSegLen * s + k) & (kWin - 1)];
   }
 };
 
@@ -129,15 +117,6 @@ hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int6
     hipLaunchKernelGGL(dev::exact_rows_kernel<dev::RawWindows<float>>, dim3(kGuardGrid),
                        dim3(kGuardBlock), 0, st, src, 16, g, out);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_guard_fixup_epochs(hipStream_t st, const double* ep, int C, int skip, int nfeat,
-                                     int row_stride, const Guard& g, double* out) {
-  if (!g.count) return hipSuccess;
-  dev::EpochWindows src{ep, row_stride, skip, C};
-  hipLaunchKernelGGL(dev::exact_rows_kernel<dev::EpochWindows>, dim3(kGuardGrid), dim3(kGuardBlock), 0,
-                     st, src, nfeat, g, out);
   return hipGetLastError();
 }
 

@@ -313,7 +313,9 @@ constexpr int kFeWin = 8 * kFeSeg;
 typedef double f64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
 
 // Under fma numerics each lane also keeps the largest |x| of its samples, and the rows are
-// checked against the conditioning guard (guard.h: sum over the channels of the measured X^2).
+// checked against the conditioning guard (guard.h: sum over the channels of the measured X^2); a
+// row that fails is recomputed under EXACT by the wave from the epochs in memory, the window LDS
+// as scratch (rare).
 template <bool FAST>
 __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* __restrict__ ep,
                                                                   int64_t n, int C, int skip,
@@ -382,6 +384,7 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
   }
   wave_sync();
   const double sx_row = __shfl(sx, (lane & 7) * 8, 64);  // epoch `lane`'s X^2 sum (lanes < 8)
+  bool fails = false;
   if (lane < ne) {
     double acc = 0.0;
     for (int i = 0; i < F; ++i) {
@@ -389,8 +392,22 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       acc = acc + f * f;  // Math.pow(f, 2) summed in index order
     }
     norm[lane] = sqrt(acc);
-    if (FAST && guard.count && guard_fails(acc, kGuardK2Collapsed, sx_row))
-      guard_flag(guard, e0 + lane);
+    fails = FAST && guard.total && guard_fails(acc, kGuardK2Collapsed, sx_row);
+  }
+  if constexpr (FAST) {  // the guard's rare path: flagged rows recomputed under EXACT in place
+    uint64_t flagged = __ballot(fails);
+    if (flagged) {
+      wave_sync();
+      if (lane == 0) atomicAdd(guard.total, (unsigned long long)__popcll(flagged));
+      do {
+        const int e = __ffsll((unsigned long long)flagged) - 1;
+        const double* row = ep + (e0 + e) * C * (int64_t)row_stride + skip;
+        dwt8_exact_row_wave([&](int c, int k) { return row[(int64_t)c * row_stride + k]; }, C,
+                            nfeat, win, feat + e * F, lane);
+        if (lane == 0) norm[e] = 1.0;  // the row is normalised
+        flagged &= flagged - 1;
+      } while (flagged);
+    }
   }
   wave_sync();
   for (int idx = lane; idx < ne * F; idx += 64) out[e0 * F + idx] = feat[idx] / norm[idx / F];
@@ -610,10 +627,6 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
   const size_t smem = sizeof(double) * (8 * (size_t)C * nfeat + 8);
   dim3 grid((unsigned)((n + 7) / 8)), block(64);
   if (fast) {
-    if (guard.count) {
-      const hipError_t e = hipMemsetAsync(guard.count, 0, sizeof(int), st);
-      if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
                        skip, nfeat, row_stride, out, guard);
   } else {

@@ -26,8 +26,8 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
                              double* out, void* scratch, int* err);
 // row_stride: doubles between consecutive (epoch, channel) rows of `ep` (750 for materialised
 // epochs, 512 for the window-only rows the host path stages)
-// guard (fma numerics): the conditioning guard's list (guard.h); its count is zeroed here and the
-// caller launches launch_guard_fixup_epochs after this kernel.
+// guard (fma numerics): the conditioning guard (guard.h); flagged rows are recomputed under EXACT
+// inside the kernel and counted in guard.total.
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,
                                        int nfeat, bool fast, double* out, int row_stride,
                                        const Guard& guard);
@@ -49,8 +49,8 @@ bool streaming_reads(int64_t n_frames, int64_t n, int64_t min_spacing);
 // the rest.
 bool fused_supported(int fmt, int ct, int C, const double* out);
 size_t fused_scratch_bytes(int64_t n, int C);
-// guard_count: zeroed by the baseline kernel (nullptr: no guard); the window kernel appends the
-// rows that fail the conditioning guard (fma) and the caller launches launch_guard_fixup_raw.
+// guard_count: zeroed by the baseline kernel when not null (the 3-channel window kernel recomputes
+// the rows that fail the fma conditioning guard itself and uses guard.total only).
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                                  void* scratch, int* err, int* guard_count);
@@ -73,13 +73,12 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
                               const void* scratch, double* out, const Guard& guard);
 
-// guard.hip: the EXACT recomputation of the rows a guarded launch flagged (no-op when
-// g.count is null).  raw: the same recording / positions / baselines (scratch) as the fused launch.
+// guard.hip: the EXACT recomputation of the rows the generic any-layout kernels flagged (no-op
+// when g.count is null; launch_window_wide issues it).  raw: the same recording / positions /
+// baselines (scratch) as the fused launch.
 hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int64_t n_frames,
                                   int ct, const ChanSel& sel, int C, const int64_t* pos,
                                   const void* scratch, const Guard& g, double* out);
-hipError_t launch_guard_fixup_epochs(hipStream_t st, const double* ep, int C, int skip, int nfeat,
-                                     int row_stride, const Guard& g, double* out);
 
 // logreg.hip: MLlib LogisticRegressionWithSGD (full batch) on device.  State block: iteration
 // count, flag (0 running, 1 converged / done, 2 invalid labels), then the d weights.

@@ -296,6 +296,7 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   __shared__ __attribute__((aligned(16))) double feat[F];
   __shared__ double norm1;
   __shared__ double gx[FAST ? C : 1];  // the guard's X^2 per channel (fma numerics)
+  __shared__ int redo;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
   const int64_t nbytes = n_frames * FB;
@@ -378,10 +379,29 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
       }
       if (lane == 0) {
         norm1 = rsqrt_nr(acc);
-        if (guard.count && guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(guard, e);
+        redo = guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
       }
     }
     __syncthreads();
+    if (redo) {  // the guard's rare path: wave 0 recomputes the row under EXACT (window LDS free)
+      if (w == 0) {
+        dwt8_exact_row_wave(
+            [&](int cc, int k) {
+              const float v = p + 175 + k < n_frames
+                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * FB + 2 * sel.col[cc])
+                                  : 0.0f;
+              float y = v * sel.res[cc];
+              y = y - base[e * C + cc];
+              return (double)y;
+            },
+            C, 16, (double*)win, feat, lane);
+        if (lane == 0) {
+          norm1 = 1.0;  // the row is normalised
+          atomicAdd(guard.total, 1ull);
+        }
+      }
+      __syncthreads();
+    }
     const double inv = norm1;
     typedef double f64x2 __attribute__((ext_vector_type(2)));
     const f64x2 v = *(const f64x2*)(feat + 2 * tid);
@@ -472,10 +492,29 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
   return hipGetLastError();
 }
 
+static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, int fmt,
+                                             int64_t n_frames, int ct, const ChanSel& sel, int C,
+                                             const int64_t* pos, int64_t n, bool fast,
+                                             const void* scratch, double* out, const Guard& guard);
+
+// The generic kernels append the rows that fail the fma guard to the list (their LDS has no room
+// for the recomputation) and the follow-up launch recomputes them (guard.hip); the 32-channel
+// kernel recomputes its own (guard.total only).
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
                               const void* scratch, double* out, const Guard& guard) {
   if (n == 0) return hipSuccess;
+  const hipError_t e = launch_window_wide_kernels(st, raw, fmt, n_frames, ct, sel, C, pos, n, fast,
+                                                  scratch, out, guard);
+  if (e != hipSuccess || !fast || !guard.count) return e;
+  if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) return hipSuccess;
+  return launch_guard_fixup_raw(st, raw, fmt, n_frames, ct, sel, C, pos, scratch, guard, out);
+}
+
+static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, int fmt,
+                                             int64_t n_frames, int ct, const ChanSel& sel, int C,
+                                             const int64_t* pos, int64_t n, bool fast,
+                                             const void* scratch, double* out, const Guard& guard) {
   const float* base = (const float*)scratch;
   const bool two = wide_lds_per_epoch(fmt, ct, C) <= 32 * 1024;  // dynamic LDS stays <= 64 KB
 #define EEGFX_W(T, FA)                                                                        \
