@@ -99,6 +99,9 @@ SIGNATURES = {
                                            c_int32, c_int32, c_int32, c_void_p, c_int]),
     "eegfx_process_recording": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p,
                                         c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int]),
+    "eegfx_process_recording_epochs": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32,
+                                               c_void_p, c_void_p, c_int32, c_void_p, c_int64,
+                                               c_void_p, c_void_p, c_int]),
     "eegfx_synth_recording": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_uint64]),
     "eegfx_logreg_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                        c_double, c_double, c_double, c_double, c_void_p,

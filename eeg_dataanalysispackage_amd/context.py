@@ -220,6 +220,29 @@ class Context:
                    n_channels_total, ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out), mem)
         return out
 
+    def process_recording_epochs(self, raw, n_channels_total: int, cols, res, pos, out=None,
+                                 epochs_out=None):
+        """getData() and extractFeatures in one pass (eegfx_process_recording_epochs): returns
+        (features [n][16*C], epochs [n][C][750]), each equal to its own call."""
+        cols_a, res_a = self._sel(cols, res)
+        raw = _raw(raw)
+        fmt = _fmt(raw)
+        n_frames = _frames(raw, n_channels_total)
+        pos = _contig(pos, np.int64)
+        n = _numel(pos)
+        C = len(cols_a)
+        if out is None:
+            out = _empty_like_mem(raw, (n, 16 * C), "float64")
+        if epochs_out is None:
+            epochs_out = _empty_like_mem(raw, (n, C, _lib.POSTSTIMULUS), "float64")
+        _check_out(out, (n, 16 * C))
+        _check_out(epochs_out, (n, C, _lib.POSTSTIMULUS))
+        mem = _mem(raw, pos, out, epochs_out)
+        self._call(mem, raw, lib().eegfx_process_recording_epochs, self.handle, ptr(raw), fmt,
+                   n_frames, n_channels_total, ptr(cols_a), ptr(res_a), C, ptr(pos), n, ptr(out),
+                   ptr(epochs_out), mem)
+        return out, epochs_out
+
     def plan_markers(self, positions, stimulus_index, n_frames: int, guessed: int,
                      balance: int = 0):
         """Marker planning (OffLineDataProvider.java:200-265) on the device as a parallel scan

@@ -338,6 +338,28 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   ctx->toc(0);
 }
 
+// raw -> epochs + features (device pointers): the one-pass kernels when the layout fits them,
+// else the cut pass followed by the batch extract over the rows it wrote.
+void run_epochs_and_features(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_frames, int ct,
+                             const ChanSel& sel, int C, const int64_t* pos, int64_t n, double* ep,
+                             double* feat) {
+  const bool fast = ctx->numerics != EEGFX_EXACT;
+  const Guard g = ctx->guard_for(n);
+  void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
+  ctx->tic();
+  if (cut_features_supported(fmt, ct, C, raw, ep, feat)) {
+    HIP_CHECK(launch_cut_features(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep, feat,
+                                  fast, fscratch, ctx->err_dev, g));
+  } else {
+    HIP_CHECK(launch_cut_epochs(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, ep, fscratch,
+                                ctx->err_dev));
+    HIP_CHECK(launch_features_from_epochs(ctx->stream, ep, n, C, EEGFX_DWT8_SKIP,
+                                          EEGFX_DWT8_FEATURE_SIZE, fast, feat, EEGFX_POSTSTIMULUS,
+                                          g));
+  }
+  ctx->toc(0);
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -361,6 +383,12 @@ struct eegfx_odp {
   void* d_epochs = nullptr;  // double[n][3][750], resident (hipMalloc, grown copy-on-grow)
   size_t d_epochs_cap = 0;
   int64_t n_epochs = 0;
+  // dwt-8 rows of the epochs, double[n][48], computed in the same pass as the epochs
+  // (eegfx_process_recording_epochs) under the numerics of the load; getFeatures() with the
+  // reference's parameters (8, 512, 175, 16) under the same numerics is then a copy
+  void* d_features = nullptr;
+  size_t d_features_cap = 0;
+  int features_numerics = -1;  // -1: no resident rows (not all epochs have them)
 
   void put_file(const std::string& k, int32_t v) {
     for (auto& kv : files)
@@ -502,12 +530,28 @@ struct eegfx_odp {
       d_epochs = np;
       d_epochs_cap = cap;
     }
+    const size_t fper = sizeof(double) * 3 * EEGFX_DWT8_FEATURE_SIZE;
+    const size_t fneed = fper * (size_t)(n_epochs + k);
+    if (fneed > d_features_cap) {
+      size_t cap = std::max(fneed, d_features_cap * 2);
+      void* np = nullptr;
+      HIP_CHECK(hipMallocAsync(&np, cap, ctx->stream));
+      if (n_epochs && features_numerics >= 0)
+        HIP_CHECK(hipMemcpyAsync(np, d_features, fper * (size_t)n_epochs, hipMemcpyDeviceToDevice,
+                                 ctx->stream));
+      if (d_features) HIP_CHECK(hipFreeAsync(d_features, ctx->stream));
+      d_features = np;
+      d_features_cap = cap;
+    }
     int64_t* d_pos = (int64_t*)ctx->pos.get(sizeof(int64_t) * (size_t)k);
     HIP_CHECK(hipMemcpyAsync(d_pos, pos.data(), sizeof(int64_t) * (size_t)k,
                              hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(launch_cut_epochs(ctx->stream, d_raw, h.info.binary_format, n_frames, ct, sel, 3,
-                                d_pos, k, (double*)((char*)d_epochs + per * (size_t)n_epochs),
-                                ctx->fused.get(fused_scratch_bytes(k, 3)), ctx->err_dev));
+    // getData()'s epochs and their dwt-8 rows in one pass over each epoch's frames
+    run_epochs_and_features(ctx, d_raw, h.info.binary_format, n_frames, ct, sel, 3, d_pos, k,
+                            (double*)((char*)d_epochs + per * (size_t)n_epochs),
+                            (double*)((char*)d_features + fper * (size_t)n_epochs));
+    if (n_epochs == 0) features_numerics = ctx->numerics;
+    else if (features_numerics != ctx->numerics) features_numerics = -1;
     ctx->drain();
     n_epochs += k;
     positions.insert(positions.end(), pos.begin(), pos.end());
@@ -850,6 +894,39 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
     run_features_from_raw(ctx, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_out);
     if (mem == EEGFX_MEM_HOST) {
       HIP_CHECK(hipMemcpyAsync(features, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      ctx->drain();
+    }
+  });
+}
+
+int eegfx_process_recording_epochs(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                                   int32_t ct, const int32_t* cols, const float* res, int32_t C,
+                                   const int64_t* pos, int64_t n, double* features,
+                                   double* epochs_out, int mem) {
+  if (!epochs_out)
+    return eegfx_process_recording(ctx, raw, fmt, n_frames, ct, cols, res, C, pos, n, features,
+                                   mem);
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    check_mem(mem);
+    if (fmt != EEGFX_INT_16 && fmt != EEGFX_IEEE_FLOAT_32) fail(EEGFX_EINVAL, "format %d", fmt);
+    if (n_frames < 0 || n < 0 || ct < 1) fail(EEGFX_EINVAL, "negative size");
+    if (n > 0 && (!raw || !pos || !features)) fail(EEGFX_EINVAL, "null buffer");
+    const ChanSel sel = make_sel(cols, res, C, ct);
+    if (mem == EEGFX_MEM_HOST) check_positions(pos, n, n_frames);
+    if (n == 0) return;
+    ctx->activate();
+    const size_t raw_bytes = (size_t)n_frames * ct * (fmt == EEGFX_INT_16 ? 2 : 4);
+    const size_t ep_bytes = sizeof(double) * (size_t)n * C * EEGFX_POSTSTIMULUS;
+    const size_t f_bytes = sizeof(double) * (size_t)n * C * EEGFX_DWT8_FEATURE_SIZE;
+    const void* d_raw = stage_in(ctx, ctx->raw, raw, raw_bytes, mem);
+    const int64_t* d_pos = (const int64_t*)stage_in(ctx, ctx->pos, pos, sizeof(int64_t) * n, mem);
+    double* d_ep = mem == EEGFX_MEM_DEVICE ? epochs_out : (double*)ctx->scratch.get(ep_bytes);
+    double* d_f = mem == EEGFX_MEM_DEVICE ? features : (double*)ctx->out.get(f_bytes);
+    run_epochs_and_features(ctx, d_raw, fmt, n_frames, ct, sel, C, d_pos, n, d_ep, d_f);
+    if (mem == EEGFX_MEM_HOST) {
+      HIP_CHECK(hipMemcpyAsync(epochs_out, d_ep, ep_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      HIP_CHECK(hipMemcpyAsync(features, d_f, f_bytes, hipMemcpyDeviceToHost, ctx->stream));
       ctx->drain();
     }
   });
@@ -1235,6 +1312,14 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
     eegfx_ctx* ctx = odp->ctx;
     ctx->activate();
     const size_t out_bytes = sizeof(double) * (size_t)odp->n_epochs * 3 * feature_size;
+    if (skip == EEGFX_DWT8_SKIP && feature_size == EEGFX_DWT8_FEATURE_SIZE &&
+        odp->features_numerics == ctx->numerics && odp->d_features) {
+      // the rows computed with the epochs at loadData (the one-pass kernels)
+      HIP_CHECK(hipMemcpyAsync(out, odp->d_features, out_bytes, hipMemcpyDeviceToHost,
+                               ctx->stream));
+      ctx->drain();
+      return;
+    }
     double* d_out = (double*)ctx->out.get(out_bytes);
     const Guard g = ctx->guard_for(odp->n_epochs);
     HIP_CHECK(launch_features_from_epochs(ctx->stream, (const double*)odp->d_epochs,
@@ -1248,9 +1333,10 @@ int eegfx_odp_get_features(eegfx_odp* odp, int32_t name, int32_t epoch_size, int
 
 void eegfx_odp_destroy(eegfx_odp* odp) {
   if (!odp) return;
-  if (odp->ctx && odp->d_epochs) {
+  if (odp->ctx && (odp->d_epochs || odp->d_features)) {
     (void)hipSetDevice(odp->ctx->device);
-    (void)hipFreeAsync(odp->d_epochs, odp->ctx->stream);
+    if (odp->d_epochs) (void)hipFreeAsync(odp->d_epochs, odp->ctx->stream);
+    if (odp->d_features) (void)hipFreeAsync(odp->d_features, odp->ctx->stream);
     (void)hipStreamSynchronize(odp->ctx->stream);
   }
   delete odp;

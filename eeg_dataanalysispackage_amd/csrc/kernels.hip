@@ -138,6 +138,102 @@ __global__ __launch_bounds__(256) void cut_write_small_kernel(
   }
 }
 
+// The one-pass getData + extractFeatures of the staged write passes (FEAT: eegfx_process_recording_
+// epochs, OffLineDataProvider.loadData then WaveletTransform.extractFeatures over its epochs,
+// OffLineDataProvider.java:216-233 + WaveletTransform.java:107-141): after the workgroup has
+// written the epoch's rows, the window frames [175, 687) are still staged in LDS, so the filter
+// bank runs on them there -- lane = (channel, segment), 8 lanes per signal, 32 signals per pass
+// of the 4 waves -- instead of a second pass that re-reads the 12 KB of window rows from HBM.
+// smp(f, col): the staged raw sample of post-stimulus frame f (zero past the recording).  The
+// decode, filter banks, normalisation and the fma guard (with its in-kernel EXACT recomputation,
+// `scratch`: 768 doubles) are those of the fused kernels.
+template <bool FAST, bool MEASURE, typename Smp>
+__device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const float* s_res,
+                                                const float* s_base, int C, double* feat,
+                                                double* gx, double* sh, double* scratch,
+                                                double* __restrict__ fo, const Guard& guard,
+                                                int tid) {
+  const int lane = tid & 63, w = tid >> 6, s = lane & 7;
+  for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
+    const int c = c0 + (lane >> 3);
+    const bool valid = c < C;
+    const int cc = valid ? c : 0;
+    const int col = s_col[cc];
+    const float r = s_res[cc], b = s_base[cc];
+    auto own = [&](int k) { return smp(175 + kSegLen * s + k, col); };
+    double a6, d6;
+    if constexpr (FAST) {
+      float ym = 0.0f;
+      dwt8_collapsed_cascade<MEASURE>(own, r, b, lane & ~7, s, a6, d6, &ym);
+      double x2;
+      if constexpr (MEASURE) {
+        const double X = (double)group8_max(ym);
+        x2 = X * X;
+      } else {
+        x2 = guard_x2_int16(r, b);
+      }
+      if (valid && s == 0) gx[c] = x2;
+    } else {
+      double a1[40];
+      level1_exact(own, r, b, lane & ~7, s, a1);
+      halo<32, true>(a1, nullptr, lane & ~7, s);
+      dwt8_levels2to6<false, true>(a1, nullptr, lane & ~7, s, a6, d6);
+    }
+    if (valid) {
+      feat[c * 16 + s] = a6;
+      feat[c * 16 + 8 + s] = d6;
+    }
+  }
+  __syncthreads();
+  const int F = 16 * C;
+  if (w == 0) {  // SignalProcessing.normalize (SignalProcessing.java:38-52)
+    if constexpr (FAST) {
+      double acc = 0.0;
+      for (int i = lane; i < F; i += 64) acc = __builtin_fma(feat[i], feat[i], acc);
+      double sx = lane < C ? gx[lane] : 0.0;  // C <= 64
+      for (int off = 32; off > 0; off >>= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        sx += __shfl_xor(sx, off, 64);
+      }
+      if (lane == 0) {
+        sh[0] = rsqrt_nr(acc);
+        sh[1] = guard.total && guard_fails(acc, kGuardK2Collapsed, sx) ? 1.0 : 0.0;
+      }
+    } else if (lane == 0) {
+      double acc = 0.0;
+      for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
+      sh[0] = sqrt(acc);
+    }
+  }
+  __syncthreads();
+  if constexpr (FAST) {
+    if (sh[1] != 0.0) {  // the guard's rare path: wave 0 recomputes the row under EXACT
+      if (w == 0) {
+        dwt8_exact_row_wave(
+            [&](int c, int k) {
+              float y = smp(175 + k, s_col[c]) * s_res[c];
+              y = y - s_base[c];
+              return (double)y;
+            },
+            C, 16, scratch, feat, lane);
+        if (lane == 0) {
+          sh[0] = 1.0;  // the row is normalised
+          atomicAdd(guard.total, 1ull);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const double nv = sh[0];
+  for (int i = tid; i < F; i += 256) fo[i] = FAST ? feat[i] * nv : feat[i] / nv;
+}
+
+// Dynamic LDS of the FEAT variants beyond the staged frames (16-byte aligned): the feature row,
+// the guard's X^2 per channel, two shared words, and the rare path's scratch (fma).
+__host__ __device__ constexpr size_t staged_features_lds(int C, bool fast) {
+  return (size_t)16 * C * 8 + 64 * 8 + 16 + (fast ? 768 * 8 : 0);
+}
+
 // The LDS-staged write pass for frames of a whole number of dwords (e.g. configs[3]'s 32-channel
 // montage; used while the staged frames are at most twice the rows written, ct <= 8 C for int16).
 // Reading one channel's samples straight from the multiplexed recording puts consecutive lanes a
@@ -157,11 +253,11 @@ __global__ __launch_bounds__(256) void cut_write_small_kernel(
 #define EEGFX_CUT_LDS_MAX (64 * 1024)
 #endif
 constexpr int kCutLdsMax = EEGFX_CUT_LDS_MAX;
-template <typename T>
+template <typename T, bool FEAT = false, bool FAST = false>
 __global__ __launch_bounds__(256) void cut_write_lds_kernel(
     const T* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
     const int64_t* __restrict__ pos, const float* __restrict__ base, double* __restrict__ out,
-    int nfc) {
+    int nfc, double* __restrict__ fout = nullptr, Guard guard = Guard{nullptr, nullptr, nullptr}) {
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
   __shared__ int s_col[kMaxChannels];
   __shared__ float s_res[kMaxChannels], s_base[kMaxChannels];
@@ -227,6 +323,17 @@ __global__ __launch_bounds__(256) void cut_write_lds_kernel(
     q += sq;
     if (q >= hp) { q -= hp; ++c; }
   }
+  if constexpr (FEAT) {  // one chunk per epoch (launcher): the window frames are staged
+    double* feat = (double*)((uint8_t*)stage + (((size_t)nf * FS * 4 + 15) & ~(size_t)15));
+    double* gx = feat + 16 * C;
+    double* sh = gx + 64;
+    staged_features<FAST, !std::is_same<T, int16_t>::value>(
+        [&](int f, int col) {
+          if constexpr (sizeof(T) == 2) return (float)((const int16_t*)stage)[2 * f * FS + col];
+          else return ((const float*)stage)[f * FS + col];
+        },
+        s_col, s_res, s_base, C, feat, gx, sh, sh + 2, fout + e * 16 * C, guard, t);
+  }
 }
 
 // The same LDS-staged write pass for int16 frames that are not a whole number of dwords (the
@@ -234,10 +341,11 @@ __global__ __launch_bounds__(256) void cut_write_lds_kernel(
 // the dword that holds its first frame, without per-frame padding; lanes reading the sample pairs
 // of one channel are 2 frames apart (3 dwords at 3 channels: an odd stride, no bank conflicts).
 // The dword holding the recording's last two bytes is read as a half so no load passes its end.
+template <bool FEAT = false, bool FAST = false>
 __global__ __launch_bounds__(256) void cut_write_lds_packed_kernel(
     const int16_t* __restrict__ raw, int64_t n_frames, int ct, ChanSel sel, int C,
     const int64_t* __restrict__ pos, const float* __restrict__ base, double* __restrict__ out,
-    int nfc) {
+    int nfc, double* __restrict__ fout = nullptr, Guard guard = Guard{nullptr, nullptr, nullptr}) {
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
   __shared__ int s_col[kMaxChannels];
   __shared__ float s_res[kMaxChannels], s_base[kMaxChannels];
@@ -292,6 +400,14 @@ __global__ __launch_bounds__(256) void cut_write_lds_packed_kernel(
     c += sc;
     q += sq;
     if (q >= hp) { q -= hp; ++c; }
+  }
+  if constexpr (FEAT) {  // one chunk per epoch (launcher): the window frames are staged
+    double* feat = (double*)((uint8_t*)stage + (((size_t)total * 4 + 15) & ~(size_t)15));
+    double* gx = feat + 16 * C;
+    double* sh = gx + 64;
+    staged_features<FAST, false>([&](int f, int col) { return (float)h[f * ct + col]; }, s_col,
+                                 s_res, s_base, C, feat, gx, sh, sh + 2, fout + e * 16 * C,
+                                 guard, t);
   }
 }
 
@@ -580,7 +696,7 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
       const int nfc = cut_chunk_frames(fbytes, 8);
       const int nchunks = (dev::kPost + nfc - 1) / nfc;
       dim3 g2((unsigned)n, (unsigned)nchunks);
-      hipLaunchKernelGGL(dev::cut_write_lds_packed_kernel, g2, block, (size_t)nfc * fbytes + 8, st,
+      hipLaunchKernelGGL(dev::cut_write_lds_packed_kernel<>, g2, block, (size_t)nfc * fbytes + 8, st,
                          (const int16_t*)raw, n_frames, ct, sel, C, pos, (const float*)scratch,
                          out, nfc);
     } else if (stage && fbytes % 4 == 0) {
@@ -618,6 +734,59 @@ hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n
     hipLaunchKernelGGL(dev::cut_epochs_kernel<float>, grid, block, 0, st, (const float*)raw,
                        n_frames, ct, sel, C, pos, out, err);
   return hipGetLastError();
+}
+
+hipError_t launch_cut_features(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                               double* out, double* feat, bool fast, void* scratch, int* err,
+                               const Guard& guard) {
+  if (!cut_features_supported(fmt, ct, C, raw, out, feat)) return hipErrorNotSupported;
+  if (n == 0) return hipSuccess;
+  hipError_t be = fmt == 0 && ct == 3 && C == 3
+                      ? launch_fused_baseline(st, raw, n_frames, ct, sel, C, pos, n, scratch, err,
+                                              nullptr)
+                      : launch_baseline_any(st, raw, fmt, n_frames, ct, sel, C, pos, n, scratch, err,
+                                            nullptr);
+  if (be != hipSuccess) return be;
+  const dim3 grid((unsigned)n), block(256);
+  const int fbytes = ct * (fmt == 0 ? 2 : 4);
+  const float* bs = (const float*)scratch;
+  const Guard g = fast ? guard : Guard{nullptr, nullptr, nullptr};
+  if (fbytes % 4 != 0) {  // int16, packed frames
+    const size_t lds = (((size_t)dev::kPost * fbytes + 8 + 15) & ~(size_t)15) +
+                       dev::staged_features_lds(C, fast);
+    if (fast)
+      hipLaunchKernelGGL((dev::cut_write_lds_packed_kernel<true, true>), grid, block, lds, st,
+                         (const int16_t*)raw, n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g);
+    else
+      hipLaunchKernelGGL((dev::cut_write_lds_packed_kernel<true, false>), grid, block, lds, st,
+                         (const int16_t*)raw, n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g);
+  } else {
+    const int fs_bytes = (fbytes / 4 + 1) * 4;
+    const size_t lds = (((size_t)dev::kPost * fs_bytes + 15) & ~(size_t)15) +
+                       dev::staged_features_lds(C, fast);
+#define EEGFX_CF(T, FA)                                                                           \
+    hipLaunchKernelGGL((dev::cut_write_lds_kernel<T, true, FA>), grid, block, lds, st, (const T*)raw, \
+                       n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g)
+    if (fmt == 0) { if (fast) EEGFX_CF(int16_t, true); else EEGFX_CF(int16_t, false); }
+    else { if (fast) EEGFX_CF(float, true); else EEGFX_CF(float, false); }
+#undef EEGFX_CF
+  }
+  return hipGetLastError();
+}
+
+// The one-pass kernels stage the whole post-stimulus span of an epoch (one chunk) plus the
+// feature row and scratch in at most 64 KB of LDS: int16 files up to ~40 channels, float32 ~20.
+bool cut_features_supported(int fmt, int ct, int C, const void* raw, const double* out,
+                            const double* feat) {
+  if (!(fmt == 0 || fmt == 1) || C < 1 || C > kMaxChannels || ct < 1) return false;
+  if (((uintptr_t)raw & 3) || ((uintptr_t)out & 15) || !feat) return false;
+  const int fbytes = ct * (fmt == 0 ? 2 : 4);
+  const size_t stage = fbytes % 4 != 0 ? (size_t)dev::kPost * fbytes + 8
+                                       : (size_t)dev::kPost * ((fbytes / 4 + 1) * 4);
+  if (fbytes % 4 != 0 && fmt != 0) return false;
+  if (!(fmt == 0 && ct == 3 && C == 3) && !baseline_any_supported(fmt, ct, C)) return false;
+  return ((stage + 15) & ~(size_t)15) + dev::staged_features_lds(C, true) <= 64 * 1024;
 }
 
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,

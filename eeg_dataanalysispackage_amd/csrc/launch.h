@@ -24,6 +24,16 @@ struct ChanSel {
 hipError_t launch_cut_epochs(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                              const ChanSel& sel, int C, const int64_t* pos, int64_t n,
                              double* out, void* scratch, int* err);
+// The one-pass getData + features (kernels.hip staged_features): baselines, then one workgroup
+// per epoch writes the epoch's rows to `out` (double[n][C][750]) and its normalised dwt-8 row to
+// `feat` (double[n][16 C]) from the same LDS-staged frames.  hipErrorNotSupported when the layout
+// does not fit (cut_features_supported): the caller cuts, then extracts from the rows.
+bool cut_features_supported(int fmt, int ct, int C, const void* raw, const double* out,
+                            const double* feat);
+hipError_t launch_cut_features(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
+                               const ChanSel& sel, int C, const int64_t* pos, int64_t n,
+                               double* out, double* feat, bool fast, void* scratch, int* err,
+                               const Guard& guard);
 // row_stride: doubles between consecutive (epoch, channel) rows of `ep` (750 for materialised
 // epochs, 512 for the window-only rows the host path stages)
 // guard (fma numerics): the conditioning guard (guard.h); flagged rows are recomputed under EXACT

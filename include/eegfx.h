@@ -211,6 +211,20 @@ int eegfx_process_recording(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_
                             int32_t C, const int64_t* pos, int64_t n_epochs, double* features,
                             int mem);
 
+/* getData() and extractFeatures in one pass (OffLineDataProvider.java:216-233 materialises the
+ * epochs, LogisticRegressionClassifier.java:87-90 then maps WaveletTransform.extractFeatures over
+ * them): the baseline-corrected epochs double[n][C][750] (epochs_out) and their dwt-8 rows
+ * double[n][16 C] (features) from one read of each epoch's frames, the filter bank running on
+ * the frames the epoch write staged.  Each output equals its own call (eegfx_cut_epochs_f64 /
+ * eegfx_process_recording), bit for bit under EEGFX_EXACT.  epochs_out == NULL: the same as
+ * eegfx_process_recording.  Layouts whose epoch span does not fit one workgroup's LDS (more than
+ * ~40 int16 / ~20 float32 channels in the file) run the two passes instead. */
+int eegfx_process_recording_epochs(eegfx_ctx* ctx, const void* raw, int32_t fmt, int64_t n_frames,
+                                   int32_t n_channels_total, const int32_t* cols,
+                                   const float* res, int32_t C, const int64_t* pos,
+                                   int64_t n_epochs, double* features, double* epochs_out,
+                                   int mem);
+
 /* configs[4] -- long recordings streamed from host memory: raw (host, n_frames x
  * n_channels_total samples), pos and features are HOST arrays; the recording is moved to the device
  * in chunks of at most chunk_frames frames (>= 787, the frames one epoch spans) on an upload

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tag", default="")
     ap.add_argument("--cut", action="store_true", help="also time eegfx_cut_epochs_f64")
+    ap.add_argument("--onepass", action="store_true",
+                    help="also time eegfx_process_recording_epochs (epochs + features in one pass) "
+                         "against the cut alone and the two passes (cut, then extract)")
     args = ap.parse_args()
     import torch
 
@@ -75,6 +78,44 @@ def main():
                           "GBps_algorithmic": round(n * bpe / (ms * 1e-3) / 1e9, 1),
                           "sha256_16": hashlib.sha256(ep.cpu().numpy().tobytes()).hexdigest()[:16]}),
               flush=True)
+    if args.onepass:
+        cols, res = list(range(C)), [0.1] * C
+        feats = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
+
+        def timed(fn):
+            for _ in range(args.warmup):
+                fn()
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(args.steps):
+                fn()
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            return a.elapsed_time(b) / args.steps
+
+        ctx.set_numerics("exact")
+        cut_ms = timed(lambda: ctx.cut_epochs(raw, C, cols, res, pos, out=ep))
+        ep_hash = hashlib.sha256(ep.cpu().numpy().tobytes()).hexdigest()[:16]
+        for numerics in ("fma", "exact"):
+            ctx.set_numerics(numerics)
+            two_ms = timed(lambda: (ctx.cut_epochs(raw, C, cols, res, pos, out=ep),
+                                    ctx.extract_features(ep, out=feats)))
+            f_two = feats.clone()
+            one_ms = timed(lambda: ctx.process_recording_epochs(raw, C, cols, res, pos, out=feats,
+                                                                epochs_out=ep))
+            ctx.synchronize()
+            print(json.dumps({
+                "tool": "epochs_bench", "tag": args.tag, "op": "epochs+features",
+                "numerics": numerics, "epochs": n, "channels": C,
+                "cut_only_ms": round(cut_ms, 4), "two_pass_ms": round(two_ms, 4),
+                "one_pass_ms": round(one_ms, 4),
+                "one_pass_over_cut": round(one_ms / cut_ms, 4),
+                "one_pass_over_two_pass": round(one_ms / two_ms, 4),
+                "epochs_equal_cut": hashlib.sha256(ep.cpu().numpy().tobytes()).hexdigest()[:16]
+                == ep_hash,
+                "features_max_abs_vs_two_pass": float((feats - f_two).abs().max())}), flush=True)
+        ctx.set_numerics("exact")
     del raw
     out = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
     results = {}
