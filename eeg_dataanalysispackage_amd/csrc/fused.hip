@@ -42,6 +42,7 @@
 #include "guard.h"
 #include "launch.h"
 #include "lds_dma.h"
+#include "rows.h"
 
 namespace eegfx {
 namespace dev {
@@ -224,89 +225,6 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
     halo<32, true>(a1, nullptr, gbase, s);
     dwt8_levels2to6<FAST, true>(a1, nullptr, gbase, s, a6, d6);
   }
-}
-
-// SignalProcessing.normalize (SignalProcessing.java:38-52) for the <= 8 feature rows of a
-// sub-tile, executed by one wave.  `fb` holds the rows in LDS; `norm` is an 8-double LDS scratch
-// owned by the calling wave.
-//   EXACT: lane e < ne folds Math.pow(f, 2) over row e in index order (the 8 dependent chains run
-//          side by side), then the 64 lanes divide and store (16-byte stores).
-//   FMA:   (1e-9 contract) the 8 lanes of an epoch each square-sum F/8 features, a 3-step
-//          butterfly completes the row sum, and the row is scaled by 1/sqrt (rsqrt_nr: within an
-//          ulp or two of x / s; an all-zero row still gives NaN = 0 * inf); the scaled rows go
-//          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
-//          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).  A row
-//          whose sum of squares fails the conditioning guard (guard.h; gx = the C per-signal X^2)
-//          is recomputed under EXACT by redo(e, row) into its row slot before the store (rare:
-//          never on the bench workload), and counted in the guard's running total.
-struct NoRedo {
-  __device__ void operator()(int, double*) const {}
-};
-template <int F, bool FAST, int C = F / 16, typename Redo = NoRedo>
-__device__ __forceinline__ void normalise_store(double* fb, double* norm, double* o, int ne,
-                                                int lane, const double* gx = nullptr,
-                                                Guard g = Guard{nullptr, nullptr, nullptr},
-                                                Redo redo = Redo{}) {
-  typedef double f64x2 __attribute__((ext_vector_type(2)));
-  if constexpr (FAST) {
-    static_assert(F % 16 == 0, "8 lanes per row, pairs of features");
-    constexpr int P = F / 8;
-    const int e = lane >> 3, p = lane & 7;
-    double v[P];
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      v[i] = e < ne ? fb[e * F + p * P + i] : 0.0;
-      acc = __builtin_fma(v[i], v[i], acc);
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    bool fails = false;
-    if (g.total && p == 0 && e < ne) {
-      double sx = 0.0;
-#pragma unroll
-      for (int c = 0; c < C; ++c) sx += gx[e * C + c];
-      fails = guard_fails(acc, kGuardK2Collapsed, sx);
-    }
-    const double inv = rsqrt_nr(acc);
-    if (e < ne) {
-#pragma unroll
-      for (int i = 0; i < P; i += 2)
-        *(double2*)(fb + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
-    }
-    wave_sync();
-    uint64_t flagged = __ballot(fails);  // bit 8e: row e failed the guard
-    if (flagged) {                        // uniform, rare
-      if (lane == 0) atomicAdd(g.total, (unsigned long long)__popcll(flagged));
-      do {
-        const int e1 = __ffsll((unsigned long long)flagged) - 1;
-        redo(e1 >> 3, fb + (e1 >> 3) * F);
-        flagged &= flagged - 1;
-      } while (flagged);
-    }
-    for (int i = 2 * lane; i < ne * F; i += 128)
-      __builtin_nontemporal_store(*(const f64x2*)(fb + i), (f64x2*)(o + i));
-    wave_sync();
-    (void)norm;
-    return;
-  }
-  if (lane < ne) {
-    double acc = 0.0;
-#pragma unroll 16
-    for (int i = 0; i < F; ++i) {
-      const double f = fb[lane * F + i];
-      acc = acc + f * f;
-    }
-    norm[lane] = sqrt(acc);
-  }
-  wave_sync();
-  for (int i = 2 * lane; i < ne * F; i += 128) {
-    const double v0 = fb[i] / norm[i / F];
-    const double v1 = fb[i + 1] / norm[(i + 1) / F];
-    *(double2*)(o + i) = make_double2(v0, v1);
-  }
-  wave_sync();
 }
 
 // DMA rows of an epoch window: each row (one global_load_lds_dwordx4, lanes < SPR * SEGQ active)

@@ -17,6 +17,7 @@
 #include "dwt8.h"
 #include "guard.h"
 #include "launch.h"
+#include "rows.h"
 
 namespace eegfx {
 namespace dev {
@@ -226,6 +227,154 @@ __device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const
   }
   const double nv = sh[0];
   for (int i = tid; i < F; i += 256) fo[i] = FAST ? feat[i] * nv : feat[i] / nv;
+}
+
+// The one-pass getData + features for the reference's 3-channel file (6-byte int16 frames, the
+// Fz/Cz/Pz selection; configs[0]-[2]): eight epochs per workgroup of four waves, so that the
+// filter bank runs with full waves -- wave c = channel c, lane = (epoch, segment), the layout of
+// the fused window kernel -- where the per-epoch staged kernel above leaves 232 of 256 lanes idle
+// (measured: one pass 8.1 ms against 7.2 ms for the two passes, profiles/r04f).
+//  1. stage: each epoch's 750 post-stimulus frames (1,127 dwords from the dword holding its first
+//     byte) go to LDS with one skew dword per 96 (every 64 frames), so the 8 segment lanes of a
+//     signal, 64 frames apart, read 8 distinct banks; epochs 1,160 dwords apart (8 mod 32).
+//  2. rows: every thread decodes sample pairs (float)raw * res - b of (epoch, channel) rows and
+//     stores them as 16-byte pairs, consecutive threads on consecutive pairs (the getData()
+//     epochs, OffLineDataProvider.java:216-233).
+//  3. features: waves 0-2 run the filter bank on the staged window frames [175, 687) (sample k of
+//     segment s: half 3 (175 + 64 s + k) + col past the epoch's start half; its skew is
+//     2 + s + [k >= 17], or [k >= 16] when the start half is odd and col = 2), then the rows are
+//     normalised and stored as in the window kernel, fma rows through the conditioning guard.
+constexpr int kCfEpochs = 8;
+constexpr int kCfDwords = 1127;  // dwords staged per epoch: (2 + 750 * 6 + 3) / 4, rounded up
+constexpr int kCfStride = 1160;  // LDS dwords per epoch: 1,127 + 12 skew dwords, = 8 (mod 32)
+__device__ __forceinline__ int cf_lds_dword(int d) { return d + (int)(((uint32_t)d * 683u) >> 16); }
+template <bool FAST>
+__global__ __launch_bounds__(256) void cut_features_c3_kernel(
+    const int16_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
+    double* __restrict__ out, double* __restrict__ fout, Guard guard) {
+  constexpr int CT = 3, C = 3, FB = 6, F = 48;
+  static_assert(kCfEpochs * F * 8 + 768 * 8 <= kCfEpochs * kCfStride * 4, "rows + scratch alias");
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kCfEpochs * kCfStride];
+  __shared__ double norm[kCfEpochs];
+  __shared__ double gx[kCfEpochs * C];
+  __shared__ int64_t sA[kCfEpochs];  // dword index of each epoch's first staged byte
+  __shared__ int sH[kCfEpochs];      // 1 when the first frame starts at an odd half
+  __shared__ int64_t sP[kCfEpochs];  // the (valid) marker position: frame of the first sample
+  __shared__ int s_col[C];
+  __shared__ float s_res[C], s_base[kCfEpochs * C];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t e0 = (int64_t)blockIdx.x * kCfEpochs;
+  const int ne = n - e0 < kCfEpochs ? (int)(n - e0) : kCfEpochs;
+  const int64_t nbytes = n_frames * FB;
+  if (tid < kCfEpochs) {
+    const int64_t p0 = tid < ne ? pos[e0 + tid] : kPre;
+    const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : kPre;  // flagged by the baselines
+    sA[tid] = (p * FB) >> 2;
+    sH[tid] = (int)((p * FB) & 3) >> 1;
+    sP[tid] = p;
+  }
+  if (tid < C) {
+    s_col[tid] = sel.col[tid];
+    s_res[tid] = sel.res[tid];
+  }
+  if (tid < kCfEpochs * C) s_base[tid] = tid < ne * C ? base[e0 * C + tid] : 0.0f;
+  __syncthreads();
+  {  // 1. stage (8 loads in flight per thread; the dword holding the recording's last two bytes
+     //    is read as a half, nothing past the end)
+    const uint32_t* src = (const uint32_t*)raw;
+    constexpr int TOTAL = kCfEpochs * kCfDwords;
+    for (int k0 = 0; k0 < TOTAL; k0 += 8 * 256) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 256 * u + tid;
+        const int m = k / kCfDwords, d = k - m * kCfDwords;
+        v[u] = 0u;
+        if (k < TOTAL && m < ne) {
+          const int64_t a = (sA[m] + d) * 4;
+          if (a + 4 <= nbytes) v[u] = src[sA[m] + d];
+          else if (a + 2 <= nbytes) v[u] = (uint16_t)raw[a >> 1];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 256 * u + tid;
+        const int m = k / kCfDwords, d = k - m * kCfDwords;
+        if (k < TOTAL) stage[m * kCfStride + cf_lds_dword(d)] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int16_t* hs = (const int16_t*)stage;
+  // staged half h of epoch m (h counted from the epoch's first staged byte)
+  auto half = [&](int m, int h) { return hs[2 * m * kCfStride + h + 2 * (int)(((uint32_t)(h >> 1) * 683u) >> 16)]; };
+  {  // 2. rows: pair q of (epoch m, channel c) = frames 2q, 2q + 1
+    constexpr int HP = kPost / 2, PER_E = C * HP;
+    int idx = tid;
+    int m = idx / PER_E, rem = idx - m * PER_E;
+    int c = rem / HP, q = rem - c * HP;
+    for (; idx < ne * PER_E; idx += 256) {
+      const int h0 = sH[m] + 6 * q + s_col[c];
+      const int64_t g = sP[m] + 2 * q;  // frame of the pair in the file
+      const float r = s_res[c], b = s_base[m * C + c];
+      // Arrays.copyOfRange zero-pads past the end (toFloatArray -> 0.0f)
+      const float v0 = g < n_frames ? (float)half(m, h0) * r : 0.0f;
+      const float v1 = g + 1 < n_frames ? (float)half(m, h0 + 3) * r : 0.0f;
+      *(double2*)(out + ((e0 + m) * C + c) * kPost + 2 * q) =
+          make_double2((double)(v0 - b), (double)(v1 - b));
+      q += 256 % HP;
+      c += 256 / HP;
+      if (q >= HP) { q -= HP; ++c; }
+      while (c >= C) { c -= C; ++m; }
+    }
+  }
+  // 3. features: wave c = channel c (waves 0-2), lane = (epoch el, segment s)
+  const int el = lane >> 3, s = lane & 7;
+  double a6 = 0.0, d6 = 0.0;
+  if (w < C) {
+    const int c = w, col = s_col[c];
+    const int m = el < ne ? el : 0;
+    const float r = s_res[c], b = s_base[m * C + c];
+    const int hb = sH[m] + col + 3 * (175 + kSegLen * s);  // half of sample 0 of this segment
+    const int16_t* own = hs + 2 * m * kCfStride + hb + 2 * (2 + s);
+    const bool late16 = sH[m] + col == 3;                 // sample 16 already past the skew
+    auto fetch = [&](int k) {
+      return (float)own[3 * k + (k >= 17 ? 2 : (k == 16 && late16 ? 2 : 0))];
+    };
+    if constexpr (FAST) {
+      dwt8_collapsed_cascade(fetch, r, b, lane & ~7, s, a6, d6);
+      if (s == 0) gx[el * C + c] = guard_x2_int16(r, b);
+    } else {
+      double a1[40];
+      level1_exact(fetch, r, b, lane & ~7, s, a1);
+      halo<32, true>(a1, nullptr, lane & ~7, s);
+      dwt8_levels2to6<false, true>(a1, nullptr, lane & ~7, s, a6, d6);
+    }
+  }
+  double* fb = (double*)stage;
+  __syncthreads();  // every wave is done with the staged frames: the rows may overwrite them
+  if (w < C) {
+    fb[el * F + w * 16 + s] = a6;
+    fb[el * F + w * 16 + 8 + s] = d6;
+  }
+  __syncthreads();
+  if (w == 0) {
+    // the guard's rare path: the row recomputed under EXACT from the recording, the LDS past the
+    // 8 rows as scratch (the other waves are done)
+    auto redo = [&](int e, double* row) {
+      const int64_t f0 = sP[e] + 175;
+      dwt8_exact_row_wave(
+          [&](int cc, int k) {
+            const float v = f0 + k < n_frames ? (float)raw[(f0 + k) * CT + s_col[cc]] : 0.0f;
+            float y = v * s_res[cc];
+            y = y - s_base[e * C + cc];
+            return (double)y;
+          },
+          C, 16, fb + kCfEpochs * F, row, lane);
+    };
+    normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo);
+  }
 }
 
 // Dynamic LDS of the FEAT variants beyond the staged frames (16-byte aligned): the feature row,
@@ -752,7 +901,15 @@ hipError_t launch_cut_features(hipStream_t st, const void* raw, int fmt, int64_t
   const int fbytes = ct * (fmt == 0 ? 2 : 4);
   const float* bs = (const float*)scratch;
   const Guard g = fast ? guard : Guard{nullptr, nullptr, nullptr};
-  if (fbytes % 4 != 0) {  // int16, packed frames
+  if (fmt == 0 && ct == 3 && C == 3) {  // the reference's file: eight epochs per workgroup
+    const dim3 g8((unsigned)((n + dev::kCfEpochs - 1) / dev::kCfEpochs));
+    if (fast)
+      hipLaunchKernelGGL(dev::cut_features_c3_kernel<true>, g8, block, 0, st, (const int16_t*)raw,
+                         n_frames, sel, pos, bs, n, out, feat, g);
+    else
+      hipLaunchKernelGGL(dev::cut_features_c3_kernel<false>, g8, block, 0, st, (const int16_t*)raw,
+                         n_frames, sel, pos, bs, n, out, feat, g);
+  } else if (fbytes % 4 != 0) {  // int16, packed frames
     const size_t lds = (((size_t)dev::kPost * fbytes + 8 + 15) & ~(size_t)15) +
                        dev::staged_features_lds(C, fast);
     if (fast)
