@@ -521,6 +521,16 @@ class _Watchdog:
             self._timer = None
 
 
+def row_checksum(rows):
+    """Order-sensitive exact checksum of a block of feature rows (torch float64 [n][F]): the rows'
+    bits as int64, weighted by their 1-based row index, summed with wraparound -- exact, so equal
+    wherever the same rows are summed; a shard moved, duplicated or altered changes it."""
+    import torch
+    bits = rows.contiguous().view(torch.int64)
+    idx = torch.arange(1, rows.shape[0] + 1, dtype=torch.int64, device=rows.device)[:, None]
+    return int((bits * idx).sum())
+
+
 def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
     """The only exchange of the path: assembling the [world*n][16C] feature matrix
     in rank (= getData()) order.  Product leg: eegfx_gather_root through the C ABI -- the matrix
@@ -547,13 +557,20 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return res, float(t[0]) * 1e3
 
+    # every rank's checksum of its own rows, gathered once (a few bytes over the process group)
+    own = torch.tensor([row_checksum(out)], dtype=torch.int64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
+    sums = [torch.zeros_like(own) for _ in range(world)]
+    dist.all_gather(sums, own)
+    sums = [int(t) for t in sums]
+
     def root_ok(full):
-        """rank 0 holds every rank's rows in rank order: its own rows bit-equal, the others unit
-        rows (each rank checks its own rows in the all-ranks legs)."""
+        """rank 0 holds every rank's rows in rank order, each shard bit-identical to what its
+        rank computed (checksums of the shards, not only unit norms: a misplaced or duplicated
+        shard fails); the other ranks receive nothing."""
         if rank != 0:
             return full is None
-        norms = torch.linalg.vector_norm(full, dim=1)
-        return bool(torch.equal(full[:n], out) and torch.max(torch.abs(norms - 1)) < 1e-12)
+        return all(row_checksum(full[r * n:(r + 1) * n]) == sums[r] for r in range(world))
 
     bpr = n * 16 * C * 8
     res = {"bytes_per_rank": bpr, "rows": world * n, "root": 0,
@@ -573,7 +590,8 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         full, ms_b = timed(lambda: comm.gather(out, world * n, out=full))
         res["all_ranks"] = {"op": "eegfx_gather (RCCL broadcast per rank, grouped)",
                             "ms": round(ms_b, 3),
-                            "rows_check": bool(torch.equal(full[rank * n:(rank + 1) * n], out))}
+                            "rows_check": all(row_checksum(full[r * n:(r + 1) * n]) == sums[r]
+                                              for r in range(world))}
         comm.close()
         del full
         got, ms_r = timed(lambda: gather_features_root(out, world * n, 0))
@@ -583,7 +601,8 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         res.update({"op": None, "ms": None, "note": "C-ABI gathers need RCCL (rehearsal backend)"})
     full, ms_t = timed(lambda: gather_features(out, world * n))
     res["torch_all_gather"] = {"ms": round(ms_t, 3),
-                               "rows_check": bool(torch.equal(full[rank * n:(rank + 1) * n], out))}
+                               "rows_check": all(row_checksum(full[r * n:(r + 1) * n]) == sums[r]
+                                                 for r in range(world))}
     del full
     if res["ms"] is None:
         res["op"], res["ms"] = "torch all_gather_into_tensor", round(ms_t, 3)

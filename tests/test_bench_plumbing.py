@@ -4,6 +4,7 @@ bench line (the GPU side is timed on the box)."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 import bench
@@ -83,3 +84,21 @@ def test_watchdog_disarmed_phase_does_not_fire():
     w.arm(0.2, None, "teardown")
     w.disarm()
     time.sleep(0.4)  # still alive: the timer was cancelled
+
+
+def test_gather_row_checksum_detects_misplaced_shards():
+    """bench.py's gather legs compare every shard on the root with its rank's own checksum
+    (unit norms alone pass a misplaced or duplicated shard)."""
+    import torch
+    rng = np.random.default_rng(3)
+    shards = [torch.from_numpy(rng.standard_normal((50, 48))) for _ in range(3)]
+    sums = [bench.row_checksum(s) for s in shards]
+    full = torch.cat(shards)
+    assert [bench.row_checksum(full[r * 50:(r + 1) * 50]) for r in range(3)] == sums
+    swapped = torch.cat([shards[1], shards[0], shards[2]])
+    assert bench.row_checksum(swapped[:50]) != sums[0]
+    dup = torch.cat([shards[0], shards[0], shards[2]])
+    assert bench.row_checksum(dup[50:100]) != sums[1]
+    rows = shards[2].clone()
+    rows[[3, 4]] = rows[[4, 3]]                       # two rows exchanged inside a shard
+    assert bench.row_checksum(rows) != sums[2]
