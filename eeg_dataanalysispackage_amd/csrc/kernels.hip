@@ -144,28 +144,33 @@ __global__ __launch_bounds__(256) void cut_write_small_kernel(
 // OffLineDataProvider.java:216-233 + WaveletTransform.java:107-141): after the workgroup has
 // written the epoch's rows, the window frames [175, 687) are still staged in LDS, so the filter
 // bank runs on them there -- lane = (channel, segment), 8 lanes per signal, 32 signals per pass
-// of the 4 waves -- instead of a second pass that re-reads the 12 KB of window rows from HBM.
-// smp(f, col): the staged raw sample of post-stimulus frame f (zero past the recording).  The
-// decode, filter banks, normalisation and the fma guard (with its in-kernel EXACT recomputation,
-// `scratch`: 768 doubles) are those of the fused kernels.
-template <bool FAST, bool MEASURE, typename Smp>
-__device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const float* s_res,
-                                                const float* s_base, int C, double* feat,
-                                                double* gx, double* sh, double* scratch,
+// of the 4 waves (C <= 64: at most two passes) -- instead of a second pass that re-reads the
+// 12 KB of window rows from HBM.  smp(f, col): the staged raw sample of post-stimulus frame f;
+// gsmp(f, col): the same sample from the recording (both zero past its end).  The decode, filter
+// banks, normalisation and the fma guard are those of the fused kernels.  The feature row and the
+// guard's rare-path scratch alias the staged frames once every wave is done with them (a barrier),
+// so the LDS stays that of the plain write pass: configs[3]'s 51 KB, three workgroups per CU.
+template <bool FAST, bool MEASURE, typename Smp, typename GSmp>
+__device__ __forceinline__ void staged_features(Smp smp, GSmp gsmp, const int* s_col,
+                                                const float* s_res, const float* s_base, int C,
+                                                double* stage, double* gx, double* sh,
                                                 double* __restrict__ fo, const Guard& guard,
                                                 int tid) {
   const int lane = tid & 63, w = tid >> 6, s = lane & 7;
-  for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
+  double a6v[2] = {0.0, 0.0}, d6v[2] = {0.0, 0.0};
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int c0 = 32 * pass + 8 * w;
+    if (c0 >= C) break;  // uniform per wave
     const int c = c0 + (lane >> 3);
     const bool valid = c < C;
     const int cc = valid ? c : 0;
     const int col = s_col[cc];
     const float r = s_res[cc], b = s_base[cc];
     auto own = [&](int k) { return smp(175 + kSegLen * s + k, col); };
-    double a6, d6;
     if constexpr (FAST) {
       float ym = 0.0f;
-      dwt8_collapsed_cascade<MEASURE>(own, r, b, lane & ~7, s, a6, d6, &ym);
+      dwt8_collapsed_cascade<MEASURE>(own, r, b, lane & ~7, s, a6v[pass], d6v[pass], &ym);
       double x2;
       if constexpr (MEASURE) {
         const double X = (double)group8_max(ym);
@@ -178,11 +183,17 @@ __device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const
       double a1[40];
       level1_exact(own, r, b, lane & ~7, s, a1);
       halo<32, true>(a1, nullptr, lane & ~7, s);
-      dwt8_levels2to6<false, true>(a1, nullptr, lane & ~7, s, a6, d6);
+      dwt8_levels2to6<false, true>(a1, nullptr, lane & ~7, s, a6v[pass], d6v[pass]);
     }
-    if (valid) {
-      feat[c * 16 + s] = a6;
-      feat[c * 16 + 8 + s] = d6;
+  }
+  __syncthreads();  // every wave is done with the staged frames: the row may overwrite them
+  double* feat = stage;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int c = 32 * pass + 8 * w + (lane >> 3);
+    if (c < C) {
+      feat[c * 16 + s] = a6v[pass];
+      feat[c * 16 + 8 + s] = d6v[pass];
     }
   }
   __syncthreads();
@@ -208,15 +219,16 @@ __device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const
   }
   __syncthreads();
   if constexpr (FAST) {
-    if (sh[1] != 0.0) {  // the guard's rare path: wave 0 recomputes the row under EXACT
+    if (sh[1] != 0.0) {  // the guard's rare path: wave 0 recomputes the row under EXACT from the
+                         // recording, the LDS past the row as scratch
       if (w == 0) {
         dwt8_exact_row_wave(
             [&](int c, int k) {
-              float y = smp(175 + k, s_col[c]) * s_res[c];
+              float y = gsmp(175 + k, s_col[c]) * s_res[c];
               y = y - s_base[c];
               return (double)y;
             },
-            C, 16, scratch, feat, lane);
+            C, 16, feat + F, feat, lane);
         if (lane == 0) {
           sh[0] = 1.0;  // the row is normalised
           atomicAdd(guard.total, 1ull);
@@ -227,6 +239,13 @@ __device__ __forceinline__ void staged_features(Smp smp, const int* s_col, const
   }
   const double nv = sh[0];
   for (int i = tid; i < F; i += 256) fo[i] = FAST ? feat[i] * nv : feat[i] / nv;
+}
+
+// LDS of the FEAT variants: the staged frames, or the feature row + the rare path's scratch that
+// alias them if larger (16-byte aligned), then the guard's X^2 per channel and two shared words.
+__host__ __device__ constexpr size_t staged_features_lds(size_t stage_bytes, int C) {
+  return (((stage_bytes > (size_t)(16 * C + 768) * 8 ? stage_bytes : (size_t)(16 * C + 768) * 8)
+           + 15) & ~(size_t)15) + 64 * 8 + 16;
 }
 
 // The one-pass getData + features for the reference's 3-channel file (6-byte int16 frames, the
@@ -378,12 +397,6 @@ __global__ __launch_bounds__(256) void cut_features_c3_kernel(
   }
 }
 
-// Dynamic LDS of the FEAT variants beyond the staged frames (16-byte aligned): the feature row,
-// the guard's X^2 per channel, two shared words, and the rare path's scratch (fma).
-__host__ __device__ constexpr size_t staged_features_lds(int C, bool fast) {
-  return (size_t)16 * C * 8 + 64 * 8 + 16 + (fast ? 768 * 8 : 0);
-}
-
 // The LDS-staged write pass for frames of a whole number of dwords (e.g. configs[3]'s 32-channel
 // montage; used while the staged frames are at most twice the rows written, ct <= 8 C for int16).
 // Reading one channel's samples straight from the multiplexed recording puts consecutive lanes a
@@ -474,15 +487,16 @@ __global__ __launch_bounds__(256) void cut_write_lds_kernel(
     if (q >= hp) { q -= hp; ++c; }
   }
   if constexpr (FEAT) {  // one chunk per epoch (launcher): the window frames are staged
-    double* feat = (double*)((uint8_t*)stage + (((size_t)nf * FS * 4 + 15) & ~(size_t)15));
-    double* gx = feat + 16 * C;
-    double* sh = gx + 64;
+    double* gx = (double*)((uint8_t*)stage + staged_features_lds((size_t)nf * FS * 4, C) - 64 * 8 - 16);
     staged_features<FAST, !std::is_same<T, int16_t>::value>(
         [&](int f, int col) {
           if constexpr (sizeof(T) == 2) return (float)((const int16_t*)stage)[2 * f * FS + col];
           else return ((const float*)stage)[f * FS + col];
         },
-        s_col, s_res, s_base, C, feat, gx, sh, sh + 2, fout + e * 16 * C, guard, t);
+        [&](int f, int col) {
+          return g0 + f < n_frames ? (float)raw[(g0 + f) * ct + col] : 0.0f;
+        },
+        s_col, s_res, s_base, C, (double*)stage, gx, gx + 64, fout + e * 16 * C, guard, t);
   }
 }
 
@@ -552,12 +566,13 @@ __global__ __launch_bounds__(256) void cut_write_lds_packed_kernel(
     if (q >= hp) { q -= hp; ++c; }
   }
   if constexpr (FEAT) {  // one chunk per epoch (launcher): the window frames are staged
-    double* feat = (double*)((uint8_t*)stage + (((size_t)total * 4 + 15) & ~(size_t)15));
-    double* gx = feat + 16 * C;
-    double* sh = gx + 64;
-    staged_features<FAST, false>([&](int f, int col) { return (float)h[f * ct + col]; }, s_col,
-                                 s_res, s_base, C, feat, gx, sh, sh + 2, fout + e * 16 * C,
-                                 guard, t);
+    double* gx = (double*)((uint8_t*)stage + staged_features_lds((size_t)total * 4, C) - 64 * 8 - 16);
+    staged_features<FAST, false>(
+        [&](int f, int col) { return (float)h[f * ct + col]; },
+        [&](int f, int col) {
+          return g0 + f < n_frames ? (float)raw[(g0 + f) * ct + col] : 0.0f;
+        },
+        s_col, s_res, s_base, C, (double*)stage, gx, gx + 64, fout + e * 16 * C, guard, t);
   }
 }
 
@@ -920,8 +935,7 @@ hipError_t launch_cut_features(hipStream_t st, const void* raw, int fmt, int64_t
       hipLaunchKernelGGL(dev::cut_features_c3_kernel<false>, g8, block, 0, st, (const int16_t*)raw,
                          n_frames, sel, pos, bs, n, out, feat, g);
   } else if (fbytes % 4 != 0) {  // int16, packed frames
-    const size_t lds = (((size_t)dev::kPost * fbytes + 8 + 15) & ~(size_t)15) +
-                       dev::staged_features_lds(C, fast);
+    const size_t lds = dev::staged_features_lds((size_t)dev::kPost * fbytes + 8, C);
     if (fast)
       hipLaunchKernelGGL((dev::cut_write_lds_packed_kernel<true, true>), grid, block, lds, st,
                          (const int16_t*)raw, n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g);
@@ -930,8 +944,7 @@ hipError_t launch_cut_features(hipStream_t st, const void* raw, int fmt, int64_t
                          (const int16_t*)raw, n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g);
   } else {
     const int fs_bytes = (fbytes / 4 + 1) * 4;
-    const size_t lds = (((size_t)dev::kPost * fs_bytes + 15) & ~(size_t)15) +
-                       dev::staged_features_lds(C, fast);
+    const size_t lds = dev::staged_features_lds((size_t)dev::kPost * fs_bytes, C);
 #define EEGFX_CF(T, FA)                                                                           \
     hipLaunchKernelGGL((dev::cut_write_lds_kernel<T, true, FA>), grid, block, lds, st, (const T*)raw, \
                        n_frames, ct, sel, C, pos, bs, out, dev::kPost, feat, g)
@@ -953,7 +966,7 @@ bool cut_features_supported(int fmt, int ct, int C, const void* raw, const doubl
                                        : (size_t)dev::kPost * ((fbytes / 4 + 1) * 4);
   if (fbytes % 4 != 0 && fmt != 0) return false;
   if (!(fmt == 0 && ct == 3 && C == 3) && !baseline_any_supported(fmt, ct, C)) return false;
-  return ((stage + 15) & ~(size_t)15) + dev::staged_features_lds(C, true) <= 64 * 1024;
+  return dev::staged_features_lds(stage, C) <= 64 * 1024;
 }
 
 hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t n, int C, int skip,

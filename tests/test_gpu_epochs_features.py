@@ -66,6 +66,7 @@ LAYOUTS = [  # (ct, cols, fmt)
     (5, [4, 1], np.int16),             # packed, 2 of 5 channels
     (4, [3, 0, 1, 2], np.int16),       # whole-dword frames
     (32, list(range(32)), np.int16),   # configs[3]'s montage: 64-byte frames
+    (40, list(range(39, -1, -1)), np.int16),  # 40 signals: two passes of the 4 waves
     (3, [2, 0, 1], np.float32),        # IEEE_FLOAT_32
     (7, [6, 5, 4, 3, 2], np.float32),
 ]

@@ -20,4 +20,9 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 10 --alt-steps 0 --same-device \
   --dist-backend gloo --no-gather > "$OUT/bench_torchrun2.json" 2> "$OUT/bench_torchrun2.err" || { tail -30 "$OUT/bench_torchrun2.err"; exit 1; }
 cat "$OUT/bench_torchrun2.json"
+echo "== torchrun 2 ranks, same device, gather legs over gloo (shard checksums)"; date
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29535 bench.py --gpus 2 --steps 5 --warmup 2 --alt-steps 0 --same-device \
+  --dist-backend gloo --epochs 20000 > "$OUT/bench_torchrun2_gather.json" 2> "$OUT/bench_torchrun2_gather.err" || { tail -30 "$OUT/bench_torchrun2_gather.err"; exit 1; }
+cat "$OUT/bench_torchrun2_gather.json"
 echo "== done"; date
