@@ -169,18 +169,25 @@ def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
 
 
 def whole_path_ceiling(C, numerics, n, step_ms, bpe):
-    """The attainable bound of the whole c3 step: baseline_kernel at its own measured time (it
+    """The attainable bound of the whole step: the baseline pass at its own measured time (it
     runs below the power cap, bound by its memory pattern) plus the window kernel's VALU bound,
-    scaled to this launch's epochs (profiles/r03_ceiling.json)."""
-    if numerics != "fma" or C != 3:
+    scaled to this launch's epochs (profiles/r03_ceiling.json): the c3 step (baseline_kernel +
+    window_kernel) and the configs[3] step (baseline_any_kernel + window_c32_kernel)."""
+    if numerics != "fma" or C not in (3, 32):
         return None
     try:
         d = json.load(open(os.path.join(REPO, CEILING_FILE)))
-        b = d["baseline_kernel<int16,3>"]["ms_alone"]
-        w = d["kernels"]["window_kernel<int16,3> fma"]
+        if C == 3:
+            base = d["baseline_kernel<int16,3>"]
+            b = base["ms_alone"] * n / base.get("epochs_per_launch", 1_000_000)
+            w = d["kernels"]["window_kernel<int16,3> fma"]
+        else:
+            base = d["baseline_any_kernel<int16> c32"]
+            b = base["ms_alone"] * n / base["epochs_per_launch"]
+            w = d["kernels"]["window_c32_kernel fma"]
     except Exception:
         return None
-    ms = (b + w["ceiling_ms"]) * n / w["epochs_per_launch"]
+    ms = b + w["ceiling_ms"] * n / w["epochs_per_launch"]
     return {"ms": round(ms, 4), "frac": round(n * bpe / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "step_over_ceiling": round(ms / step_ms, 4),
             "baseline_kernel_ms_alone": b, "source": CEILING_FILE}
