@@ -60,7 +60,15 @@ def test_whole_path_ceiling_adds_the_baseline_pass():
     assert c["ms"] == pytest.approx(b + w, abs=1e-4)
     assert c["frac"] == pytest.approx(4.064e9 / ((b + w) * 1e-3) / 8e12, rel=1e-3)
     assert 0.5 < c["frac"] < 0.8
-    assert bench.whole_path_ceiling(32, "fma", 1, 1.0, 1) is None
+    # configs[3]: baseline_any_kernel's measured time + the 32-channel window kernel's bound
+    b32 = d["baseline_any_kernel<int16> c32"]
+    w32 = d["kernels"]["window_c32_kernel fma"]
+    n = w32["epochs_per_launch"]
+    c32 = bench.whole_path_ceiling(32, "fma", n, 2.0, 43272)
+    assert c32["ms"] == pytest.approx(b32["ms_alone"] * n / b32["epochs_per_launch"]
+                                      + w32["ceiling_ms"], abs=1e-4)
+    assert 0.5 < c32["frac"] < 0.9
+    assert bench.whole_path_ceiling(16, "fma", 1, 1.0, 1) is None
     assert bench.whole_path_ceiling(3, "exact", 1, 1.0, 1) is None
 
 
