@@ -384,7 +384,7 @@ __device__ __forceinline__ void dwt8_fast_cascade(Fetch fetch, float r, float b,
 // -1.  Over all pairs the lane accumulates A0 += B0 x1, Ai += B2 x0, Bp += (B0 + B1 + B2)/2 (x1 + x0)
 // and Bm += (B0 - B1 + B2)/2 (x1 - x0), three entries each, and interpolates once:
 // c0 = A0, c3 = Ai, c1 = Bp - Bm - c3, c2 = Bp + Bm - c0, P[3q + r] = c_r[q] (+ c3[q - 1] for r = 0).
-// That is 12 multiply-adds and two exact adds (x1 +- x0, two floats) per pair, 11 + 2 once tap 280
+// That is 12 multiply-adds and two adds (x1 +- x0, nearly always exact) per pair, 11 + 2 once tap 280
 // is passed: 440 per lane instead of the direct form's 560.  The constants are exact rational sums
 // halved and rounded once (dwt8_taps.h), one 96-byte row per pair.
 //   Measured: the two-term Karatsuba form (464 per lane, `git show
@@ -418,7 +418,11 @@ __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, 
     if (n + 2 < 32) { vq[n % 2][0] = fetch(n + 2); vq[n % 2][1] = fetch(n + 2 + 32); }
     double x0, x1;
     decode(v0, v1, x0, x1);
-    const double xp = x1 + x0, xm = x1 - x0;  // exact: two floats
+    // exact when the pair's exponents lie within 29 of each other (the decoded fp32 samples of a
+    // window nearly always do); otherwise, and for caller-supplied doubles
+    // (features_from_epochs_kernel), one rounding each -- tools/fma_bound.py models both adds as
+    // rounded, so the guard's bound covers either case
+    const double xp = x1 + x0, xm = x1 - x0;
     const const_f64_ptr R = tab + n * kH5Cols;  // this pair's 12 constants (96 bytes)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {

@@ -102,7 +102,7 @@ def test_device_cut_epochs_small_and_wide(ctxs, fmt, cols):
     ("int16", 3, [0, 1, 2]),                  # 6-byte frames: the packed staging (configs[1])
     ("int16", 3, [2, 0]),
     ("int16", 7, [3]),                        # 14-byte frames, one channel of seven
-    ("float32", 32, list(range(0, 32, 2))),   # 32 dwords per frame: four chunks per epoch
+    ("float32", 32, list(range(0, 32, 2))),   # 33 staged dwords per frame: two chunks per epoch
     ("float32", 5, [4, 3, 2, 1, 0]),
 ])
 def test_device_cut_epochs_lds_staged(ctxs, fmt, ct, cols):
