@@ -42,6 +42,12 @@
 #define EEGFX_COLLAPSED 1
 #endif
 
+// The fma numerics' conditioning guard in the window kernels (guard.h); 0 only in A/B probe builds
+// (tools/probes/ablations/noguard.patch) that measure its cost.
+#ifndef EEGFX_GUARD
+#define EEGFX_GUARD 1
+#endif
+
 namespace eegfx {
 namespace dev {
 

@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   const bool mine = el < ne;
   const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
   const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
-  if (FAST && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
+  if (FAST && EEGFX_GUARD && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
   const DmaRows<CT> rows(lane);
   if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
     dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);

@@ -49,7 +49,7 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
     bool fails = false;
-    if (g.total && p == 0 && e < ne) {
+    if (EEGFX_GUARD && g.total && p == 0 && e < ne) {
       double sx = 0.0;
 #pragma unroll
       for (int c = 0; c < C; ++c) sx += gx[e * C + c];

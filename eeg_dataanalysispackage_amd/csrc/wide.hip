@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   }
   feat[c * 16 + s] = a6;
   feat[c * 16 + 8 + s] = d6;
-  if (FAST && s == 0) gx[c] = guard_x2_int16(r, b);
+  if (FAST && EEGFX_GUARD && s == 0) gx[c] = guard_x2_int16(r, b);
   __syncthreads();
   double* o = out + e * F;
   if constexpr (FAST) {
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
       }
       if (lane == 0) {
         norm1 = rsqrt_nr(acc);
-        redo = guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
+        redo = EEGFX_GUARD && guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
       }
     }
     __syncthreads();

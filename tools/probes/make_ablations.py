@@ -30,6 +30,10 @@ FMA_BODY = """#pragma unroll
     }"""
 
 ABLATIONS = {
+    "noguard": (
+        "the fma conditioning guard compiled out of the window kernels (no per-signal X^2, no "
+        "per-row check, no rare path): A/B of its cost (round 4)",
+        [("dwt8.h", "#define EEGFX_GUARD 1", "#define EEGFX_GUARD 0")]),
     "cascade": (
         "fma filter bank as the round-2 level-by-level cascade with partial-sum halos "
         "(A/B against the collapsed filter)",

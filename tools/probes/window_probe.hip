@@ -30,6 +30,7 @@
 #include FUSED_SRC
 #include WIDE_SRC
 #include "../../eeg_dataanalysispackage_amd/csrc/kernels.hip"
+#include "../../eeg_dataanalysispackage_amd/csrc/guard.hip"
 
 int main() {
   const bool wide = getenv("PROBE_WIDE") != nullptr;
@@ -50,13 +51,21 @@ int main() {
   (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
   eegfx::ChanSel sel{};
   for (int c = 0; c < ct; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
+  // the product's fma guard state (eegfx_ctx: count, running total, list)
+  int* gdev;
+  int64_t* glist;
+  (void)hipMalloc(&gdev, 16);
+  (void)hipMemset(gdev, 0, 16);
+  (void)hipMalloc(&glist, n * 8);
+  const eegfx::Guard g = fast ? eegfx::Guard{gdev, glist, (unsigned long long*)(gdev + 2)}
+                              : eegfx::Guard{nullptr, nullptr, nullptr};
   auto baseline = [&] {
-    if (wide) (void)eegfx::launch_baseline_any(0, raw, 0, nf, ct, sel, ct, pos, n, base, nullptr);
-    else (void)eegfx::launch_fused_baseline(0, raw, nf, ct, sel, ct, pos, n, base, nullptr);
+    if (wide) (void)eegfx::launch_baseline_any(0, raw, 0, nf, ct, sel, ct, pos, n, base, nullptr, g.count);
+    else (void)eegfx::launch_fused_baseline(0, raw, nf, ct, sel, ct, pos, n, base, nullptr, nullptr);
   };
   auto window = [&] {
-    if (wide) (void)eegfx::launch_window_wide(0, raw, 0, nf, ct, sel, ct, pos, n, fast, base, out);
-    else (void)eegfx::launch_fused_window(0, raw, nf, ct, sel, ct, pos, n, fast, base, out);
+    if (wide) (void)eegfx::launch_window_wide(0, raw, 0, nf, ct, sel, ct, pos, n, fast, base, out, g);
+    else (void)eegfx::launch_fused_window(0, raw, nf, ct, sel, ct, pos, n, fast, base, out, g);
   };
   baseline();
   const char* it = getenv("PROBE_ITERS");
