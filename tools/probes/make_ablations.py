@@ -29,7 +29,35 @@ FMA_BODY = """#pragma unroll
       Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
     }"""
 
+BASELINE_T32 = [
+    ("fused.hip", "  const dim3 g((unsigned)((n + 63) / 64));",
+     "  const dim3 g((unsigned)((n + 31) / 32));  // ablation: 32-epoch tiles"),
+    ("fused.hip", """    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,""",
+     """    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 32, true>), g, dim3(128), 0, st,"""),
+    ("fused.hip", """    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,""",
+     """    hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 32>), g, dim3(128), 0, st, (const uint8_t*)raw,"""),
+]
+
 ABLATIONS = {
+    "baseline32": (
+        "baseline_kernel on 32-epoch tiles (the reference point of baseline128: same LDS "
+        "occupancy class)",
+        BASELINE_T32),
+    "baseline128": (
+        "baseline_kernel staging whole 128-byte lines: each epoch's quads start at floor128 of its "
+        "600-byte run and cover only the lines the run touches (VERDICT r03 item 5), 32-epoch tiles",
+        BASELINE_T32 + [
+            ("fused.hip",
+             "  static constexpr int BASEQ = (kPre * FB + 15) / 16 + 1;    // 39 quads (600 B + misalignment)",
+             "  static constexpr int BASEQ = (kPre * FB + 127) / 128 * 8 + 8;  // ablation: whole lines"),
+            ("fused.hip",
+             "    A[k] = want[k] ? (tB[e] & ~(int64_t)15) + 16 * q : 0;",
+             "    want[k] = want[k] && 16 * q < (int)(((tB[e] & 127) + kPre * G::FB + 127) & ~127);\n"
+             "    A[k] = want[k] ? (tB[e] & ~(int64_t)127) + 16 * q : 0;"),
+            ("fused.hip",
+             "  const int16_t* src = (const int16_t*)((const uint8_t*)(stage + e * G::BSTR) + (tB[e] & 15)) +",
+             "  const int16_t* src = (const int16_t*)((const uint8_t*)(stage + e * G::BSTR) + (tB[e] & 127)) +"),
+        ]),
     "noguard": (
         "the fma conditioning guard compiled out of the window kernels (no per-signal X^2, no "
         "per-row check, no rare path): A/B of its cost (round 4)",
