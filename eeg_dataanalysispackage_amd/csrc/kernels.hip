@@ -591,13 +591,19 @@ __global__ __launch_bounds__(256) void cut_write_lds_packed_kernel(
 // workgroup: 4 workgroups per CU.
 constexpr int kFeSeg = kSegLen + 1;
 constexpr int kFeWin = 8 * kFeSeg;
+constexpr size_t kFeWinBytes = sizeof(double) * 8 * kFeWin;
 typedef double f64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
 
 // Under fma numerics each lane also keeps the largest |x| of its samples, and the rows are
 // checked against the conditioning guard (guard.h: sum over the channels of the measured X^2); a
 // row that fails is recomputed under EXACT by the wave from the epochs in memory, the window LDS
 // as scratch (rare).
-template <bool FAST>
+// ROWS_OUT (wide rows, launcher): the 8 feature rows (8 F doubles: 32 KB at C = 32) do not stay in
+// LDS, where they halved the resident workgroups.  After each channel the 8 x nfeat values pass
+// through a 1 KB LDS tile, leave as whole 128-byte runs into `out`, and lanes 0-7 add their
+// squares to the epoch's sum in index order (the reference's sequential sum,
+// SignalProcessing.java:38-52); at the end the wave rescales its rows in place (L2-resident).
+template <bool FAST, bool ROWS_OUT>
 __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* __restrict__ ep,
                                                                   int64_t n, int C, int skip,
                                                                   int nfeat, int row_stride,
@@ -608,10 +614,11 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
   const int lane = threadIdx.x;
   const int el = lane >> 3, s = lane & 7;
   const int F = C * nfeat;
-  double* feat = fsmem;         // [8][F]
-  double* norm = feat + 8 * F;  // [8]
+  double* feat = fsmem;                             // [8][F], or the [8][16] tile (ROWS_OUT)
+  double* norm = feat + (ROWS_OUT ? 8 * 16 : 8 * F);  // [8]
   const int64_t e0 = (int64_t)blockIdx.x * 8;
   const int64_t ne = (n - e0) < 8 ? (n - e0) : 8;
+  double* o = out + e0 * F;
   // quad q = 64 (j % 4) + lane of window j / 4: doubles 2q, 2q + 1 of segment q / 32.  Epochs
   // past n read the last epoch's window (the loads stay unconditional; the result is dropped).
   // Channel c + 1's windows are in flight while channel c runs the filter bank.
@@ -622,11 +629,12 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       const int g = j >> 2;
       const int64_t e = e0 + (g < ne ? g : ne - 1);
       const int q = ((j & 3) << 6) | lane;
-      v[j] = *(const f64x2_a8*)(ep + (e * C + c) * row_stride + skip + 2 * q);
+      v[j] = __builtin_nontemporal_load((const f64x2_a8*)(ep + (e * C + c) * row_stride + skip + 2 * q));
     }
   };
   load(0);
-  double sx = 0.0;  // fma: sum over the channels of this lane's signal's X^2
+  double sx = 0.0;   // fma: sum over the channels of this lane's signal's X^2
+  double acc = 0.0;  // ROWS_OUT, lanes < ne: epoch `lane`'s sum of squares so far
   for (int c = 0; c < C; ++c) {
     wave_sync();  // the previous channel's LDS reads precede these writes
 #pragma unroll
@@ -658,7 +666,20 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       for (int k = 0; k < kIn; ++k) x[k] = k < kSegLen ? own[k] : sig[((s + 1) & 7) * kFeSeg + k - kSegLen];
       dwt8_cascade<false, true>(x, nullptr, lane & ~7, s, a6, d6);
     }
-    if (el < ne) {
+    if constexpr (ROWS_OUT) {
+      feat[el * 16 + s] = a6;  // the tile's previous reads finished before the window writes
+      feat[el * 16 + 8 + s] = d6;
+      wave_sync();
+      for (int idx = lane; idx < ne * nfeat; idx += 64) {
+        const int e = idx / nfeat, j = idx - e * nfeat;
+        o[(int64_t)e * F + c * nfeat + j] = feat[e * 16 + j];
+      }
+      if (lane < ne)
+        for (int j = 0; j < nfeat; ++j) {
+          const double f = feat[lane * 16 + j];
+          acc = acc + f * f;  // Math.pow(f, 2) summed in index order
+        }
+    } else if (el < ne) {
       if (s < nfeat) feat[el * F + c * nfeat + s] = a6;
       if (8 + s < nfeat) feat[el * F + c * nfeat + 8 + s] = d6;
     }
@@ -667,10 +688,11 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
   const double sx_row = __shfl(sx, (lane & 7) * 8, 64);  // epoch `lane`'s X^2 sum (lanes < 8)
   bool fails = false;
   if (lane < ne) {
-    double acc = 0.0;
-    for (int i = 0; i < F; ++i) {
-      const double f = feat[lane * F + i];
-      acc = acc + f * f;  // Math.pow(f, 2) summed in index order
+    if constexpr (!ROWS_OUT) {
+      for (int i = 0; i < F; ++i) {
+        const double f = feat[lane * F + i];
+        acc = acc + f * f;  // Math.pow(f, 2) summed in index order
+      }
     }
     norm[lane] = sqrt(acc);
     fails = FAST && guard.total && guard_fails(acc, kGuardK2Collapsed, sx_row);
@@ -683,15 +705,42 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       do {
         const int e = __ffsll((unsigned long long)flagged) - 1;
         const double* row = ep + (e0 + e) * C * (int64_t)row_stride + skip;
+        double* dst = ROWS_OUT ? win + 768 : feat + e * F;  // ROWS_OUT: F <= 64 x 16 fits
         dwt8_exact_row_wave([&](int c, int k) { return row[(int64_t)c * row_stride + k]; }, C,
-                            nfeat, win, feat + e * F, lane);
+                            nfeat, win, dst, lane);
+        if constexpr (ROWS_OUT) {
+          wave_sync();
+          for (int i = lane; i < F; i += 64) o[(int64_t)e * F + i] = dst[i];
+          wave_sync();
+        }
         if (lane == 0) norm[e] = 1.0;  // the row is normalised
         flagged &= flagged - 1;
       } while (flagged);
     }
   }
   wave_sync();
-  for (int idx = lane; idx < ne * F; idx += 64) out[e0 * F + idx] = feat[idx] / norm[idx / F];
+  if constexpr (ROWS_OUT) {
+    __threadfence_block();  // this wave's raw rows are complete before it reads them back
+    for (int e = 0; e < ne; ++e) {  // eight loads in flight per batch (L2 round trips)
+      double* r = o + (int64_t)e * F;
+      const double nv = norm[e];
+      for (int i0 = 0; i0 < F; i0 += 8 * 64) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + 64 * u + lane;
+          t[u] = i < F ? r[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + 64 * u + lane;
+          if (i < F) r[i] = t[u] / nv;
+        }
+      }
+    }
+  } else {
+    for (int idx = lane; idx < ne * F; idx += 64) o[idx] = feat[idx] / norm[idx / F];
+  }
 }
 
 // a11..a13 for small host batches (the per-epoch IFeatureExtraction drop-in): one workgroup per
@@ -973,15 +1022,21 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
                                        int nfeat, bool fast, double* out, int row_stride,
                                        const Guard& guard) {
   if (n == 0) return hipSuccess;
-  const size_t smem = sizeof(double) * (8 * (size_t)C * nfeat + 8);
+  // The rows stay in LDS while the workgroup (33 KB of windows + 8 rows) still fits three times
+  // per CU (C <= 20 at 16 features); wider rows go through `out`, which keeps four per CU.
+  // Measured (profiles/r04q/, fma / EXACT): C = 24 rows in LDS 2.86 / 3.52 ms, through `out`
+  // 2.61 / 2.77 ms; C = 32 2.88 / 3.53 vs 2.82 / 2.96 ms; C = 16 2.40 / 2.54 vs 2.57 / 2.72 ms.
+  const size_t lds_rows = dev::kFeWinBytes + sizeof(double) * (8 * (size_t)C * nfeat + 8);
+  const bool rows_out = 3 * lds_rows > 160 * 1024;
+  const size_t smem = sizeof(double) * (rows_out ? 8 * 16 + 8 : 8 * (size_t)C * nfeat + 8);
   dim3 grid((unsigned)((n + 7) / 8)), block(64);
-  if (fast) {
-    hipLaunchKernelGGL(dev::features_from_epochs_kernel<true>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, row_stride, out, guard);
-  } else {
-    hipLaunchKernelGGL(dev::features_from_epochs_kernel<false>, grid, block, smem, st, ep, n, C,
-                       skip, nfeat, row_stride, out, Guard{nullptr, nullptr, nullptr});
-  }
+  const Guard none{nullptr, nullptr, nullptr};
+#define EEGFX_FFE(FA, RO)                                                                         \
+  hipLaunchKernelGGL((dev::features_from_epochs_kernel<FA, RO>), grid, block, smem, st, ep, n, C,  \
+                     skip, nfeat, row_stride, out, FA ? guard : none)
+  if (fast) { if (rows_out) EEGFX_FFE(true, true); else EEGFX_FFE(true, false); }
+  else { if (rows_out) EEGFX_FFE(false, true); else EEGFX_FFE(false, false); }
+#undef EEGFX_FFE
   return hipGetLastError();
 }
 

@@ -3,8 +3,9 @@ WaveletTransform.extractFeatures on double[n][C][750], WaveletTransform.java:107
 getData() write passes cut_write_small_kernel / cut_write_kernel (OffLineDataProvider.java:216-233).
 
 The batch extractor stages eight windows per channel through LDS and, under fma numerics, runs the
-collapsed four-point filter on the doubles; its feature rows sit in dynamic LDS (8 x 16C doubles, 64
-KB at C = 64).  Ragged tiles (n not a multiple of 8) read the last epoch's windows and drop the
+collapsed four-point filter on the doubles; its feature rows sit in dynamic LDS (8 x 16C doubles)
+while the workgroup still fits three times per CU (C <= 20), and go through the output rows beyond
+(C = 21, 32, 64: rescaled in place at the end).  Ragged tiles (n not a multiple of 8) read the last epoch's windows and drop the
 result.  EXACT must equal the oracle value for value; fma within 1e-9 per normalised feature (the
 north_star tolerance).  Inputs are random doubles, not only decoded int16 epochs, since the API
 takes any double rows."""
@@ -29,7 +30,7 @@ def eq(a, b):
     return np.array_equal(a, b, equal_nan=True)
 
 
-@pytest.mark.parametrize("C", [1, 2, 5, 17, 64])
+@pytest.mark.parametrize("C", [1, 2, 5, 17, 20, 21, 32, 64])
 @pytest.mark.parametrize("n", [1, 7, 9, 33])
 def test_device_batch_extract(ctxs, C, n):
     import torch
@@ -45,11 +46,12 @@ def test_device_batch_extract(ctxs, C, n):
     assert np.max(np.abs(got_f - want)) <= 1e-9, (C, n)
 
 
-@pytest.mark.parametrize("nf,skip", [(1, 0), (8, 100), (16, 238)])
-def test_device_batch_extract_feature_size_and_skip(ctxs, nf, skip):
+@pytest.mark.parametrize("C", [3, 32])
+@pytest.mark.parametrize("nf,skip", [(1, 0), (8, 100), (12, 5), (16, 238)])
+def test_device_batch_extract_feature_size_and_skip(ctxs, nf, skip, C):
     import torch
-    rng = np.random.default_rng(nf + skip)
-    ep = rng.standard_normal((21, 3, 750))
+    rng = np.random.default_rng(nf + skip + C)
+    ep = rng.standard_normal((21, C, 750))
     want = oracle.extract_features(ep, nfeat=nf, skip=skip)
     exact, fma = ctxs
     dep = torch.from_numpy(ep).cuda()

@@ -152,7 +152,8 @@ def test_dc_plus_alternating_and_near_null(ctx):
 
 def test_null_space_every_fma_kernel_family(ctx):
     """The guard in each fma kernel: any-layout (ct=5), the 32-channel montage, float32
-    recordings (measured X), device batch extract, per-epoch host extract, streamed."""
+    recordings (measured X), device batch extract (rows in LDS and, at C = 32, through the
+    output), per-epoch host extract, streamed."""
     import torch
     n = 24
     pos = np.arange(1000, 1000 * (n + 1), 1000, dtype=np.int64) + np.arange(n) % 2
@@ -174,6 +175,18 @@ def test_null_space_every_fma_kernel_family(ctx):
     assert eq(ctx.extract_features(torch.from_numpy(ep).cuda()).cpu().numpy(), want)
     assert eq(ctx.extract_features(ep), want)                # host batch (chunked copies)
     assert eq(ctx.extract_features(ep[:5]), want[:5])        # per-epoch drop-in kernel
+    # wide rows (C = 32: the batch extract's rows go through `out`), flagged rows mixed with
+    # ordinary ones in one tile
+    wide = alternating(1000 * 20 + 2000, 32, 700, 0)
+    ep32 = oracle.decode_epochs(wide, list(range(32)), [0.1] * 32, posm[:20])
+    ep32[1::3] += np.random.default_rng(3).standard_normal((7, 32, 750))
+    want32 = oracle.extract_features(ep32)
+    ctx.guard_stats(reset=True)
+    got32 = ctx.extract_features(torch.from_numpy(ep32).cuda()).cpu().numpy()
+    flagged = [i for i in range(20) if i % 3 != 1]
+    assert eq(got32[flagged], want32[flagged])
+    assert np.max(np.abs(got32 - want32)) <= 1e-9
+    assert ctx.guard_stats()[1] == len(flagged)
     wt = fx.WaveletTransform(8, 512, 175, 16, context=ctx)
     assert eq(wt.extractFeatures(ep[3]), want[3])
     want = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
