@@ -705,7 +705,8 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
       do {
         const int e = __ffsll((unsigned long long)flagged) - 1;
         const double* row = ep + (e0 + e) * C * (int64_t)row_stride + skip;
-        double* dst = ROWS_OUT ? win + 768 : feat + e * F;  // ROWS_OUT: F <= 64 x 16 fits
+        static_assert(768 + kMaxChannels * 16 <= 8 * kFeWin, "the recomputed row fits the windows");
+        double* dst = ROWS_OUT ? win + 768 : feat + e * F;  // past the 768-double scratch
         dwt8_exact_row_wave([&](int c, int k) { return row[(int64_t)c * row_stride + k]; }, C,
                             nfeat, win, dst, lane);
         if constexpr (ROWS_OUT) {
