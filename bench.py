@@ -571,13 +571,21 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
     dist.all_gather(sums, own)
     sums = [int(t) for t in sums]
 
+    def every_rank(flag):
+        """True when `flag` holds on every rank (a MIN over the process group)."""
+        t = torch.tensor([1 if flag else 0], dtype=torch.int64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(int(t[0]))
+
     def root_ok(full):
         """rank 0 holds every rank's rows in rank order, each shard bit-identical to what its
         rank computed (checksums of the shards, not only unit norms: a misplaced or duplicated
-        shard fails); the other ranks receive nothing."""
+        shard fails); the other ranks receive nothing -- checked on every rank."""
         if rank != 0:
-            return full is None
-        return all(row_checksum(full[r * n:(r + 1) * n]) == sums[r] for r in range(world))
+            return every_rank(full is None)
+        return every_rank(all(row_checksum(full[r * n:(r + 1) * n]) == sums[r]
+                              for r in range(world)))
 
     bpr = n * 16 * C * 8
     res = {"bytes_per_rank": bpr, "rows": world * n, "root": 0,
@@ -597,8 +605,9 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         full, ms_b = timed(lambda: comm.gather(out, world * n, out=full))
         res["all_ranks"] = {"op": "eegfx_gather (RCCL broadcast per rank, grouped)",
                             "ms": round(ms_b, 3),
-                            "rows_check": all(row_checksum(full[r * n:(r + 1) * n]) == sums[r]
-                                              for r in range(world))}
+                            "rows_check": every_rank(all(
+                                row_checksum(full[r * n:(r + 1) * n]) == sums[r]
+                                for r in range(world)))}
         comm.close()
         del full
         got, ms_r = timed(lambda: gather_features_root(out, world * n, 0))
@@ -608,8 +617,9 @@ def bench_gather(args, ctx, out, n, C, rank, world, dev, dist):
         res.update({"op": None, "ms": None, "note": "C-ABI gathers need RCCL (rehearsal backend)"})
     full, ms_t = timed(lambda: gather_features(out, world * n))
     res["torch_all_gather"] = {"ms": round(ms_t, 3),
-                               "rows_check": all(row_checksum(full[r * n:(r + 1) * n]) == sums[r]
-                                                 for r in range(world))}
+                               "rows_check": every_rank(all(
+                                   row_checksum(full[r * n:(r + 1) * n]) == sums[r]
+                                   for r in range(world)))}
     del full
     if res["ms"] is None:
         res["op"], res["ms"] = "torch all_gather_into_tensor", round(ms_t, 3)
