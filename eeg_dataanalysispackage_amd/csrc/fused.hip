@@ -343,12 +343,18 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   const int ne = (rest >> 31) != 0 ? kSub : ((int)rest < kSub ? (int)rest : kSub);
 
   const bool mine = el < ne;
-  const float b = mine ? base[(e0 + el) * C + w] : 0.0f;
-  const int delta = mine ? (int)((uint32_t)wb[e0 + el] & 14u) : 0;
-  if (FAST && EEGFX_GUARD && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
+  // This lane's baseline and window word: loaded unconditionally (clamped to a valid epoch) and
+  // used only once the window DMAs are in flight, so the prologue waits on one round trip (the
+  // window words' scalar loads) before the DMAs leave instead of three.
+  const int elc = mine ? el : ne - 1;
+  const float b_ld = base[(e0 + elc) * C + w];
+  const uint32_t w_ld = (uint32_t)wb[e0 + elc];
   const DmaRows<CT> rows(lane);
   if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
     dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  const float b = mine ? b_ld : 0.0f;
+  const int delta = mine ? (int)(w_ld & 14u) : 0;
+  if (FAST && EEGFX_GUARD && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
   dma_drain();
   __syncthreads();
 

@@ -17,8 +17,7 @@ CSRC = os.path.join(HERE, "..", "..", "eeg_dataanalysispackage_amd", "csrc")
 FILES = ("fused.hip", "wide.hip", "dwt8.h")
 
 DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
-    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
-  dma_drain();"""
+    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);"""
 
 FMA_BODY = """#pragma unroll
     for (int q = 0; q < 3; ++q) {
