@@ -8,7 +8,7 @@ for rep in $(seq 1 ${REPS:-3}); do
 import sys, runpy
 import eeg_dataanalysispackage_amd._lib as L
 L.LIB_PATH = '$lib'
-sys.argv = ['bench.py', '--workload', '${WL:-c3}', '--steps', '${STEPS:-200}', '--warmup', '20', '--alt-steps', '0', '--cpu-sample', '0']
+sys.argv = ['bench.py', '--workload', '${WL:-c3}', '--steps', '${STEPS:-200}', '--warmup', '20', '--alt-steps', '0', '--cpu-sample', '0'] + '${ARGS:-}'.split()
 runpy.run_path('bench.py', run_name='__main__')
 " >> gpurun_out/${TAG:-r04x}/ab.log 2>/dev/null || exit 1
   done
