@@ -143,11 +143,11 @@ def traffic_from_profiles(workload_key):
     return best
 
 
-CEILING_FILE = os.path.join("profiles", "r03_ceiling.json")
+CEILING_FILE = os.path.join("profiles", "r04_ceiling.json")
 
 
 def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
-    """The attainable bound of the dominant kernel (profiles/r03_ceiling.json, written by
+    """The attainable bound of the dominant kernel (profiles/r04_ceiling.json, written by
     tools/ceiling_summary.py): its VALU issue time at the clock the chip holds under the kernel's
     own sustained power draw (SQ counters + amd-smi under load), scaled to this launch's epochs,
     next to the live kernel time."""
@@ -171,7 +171,7 @@ def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
 def whole_path_ceiling(C, numerics, n, step_ms, bpe):
     """The attainable bound of the whole step: the baseline pass at its own measured time (it
     runs below the power cap, bound by its memory pattern) plus the window kernel's VALU bound,
-    scaled to this launch's epochs (profiles/r03_ceiling.json): the c3 step (baseline_kernel +
+    scaled to this launch's epochs (profiles/r04_ceiling.json): the c3 step (baseline_kernel +
     window_kernel) and the configs[3] step (baseline_any_kernel + window_c32_kernel)."""
     if numerics != "fma" or C not in (3, 32):
         return None
