@@ -7,7 +7,8 @@ Per case: a random recording (int16 / float32, 1-64 channels per frame, any sele
 legal edges (pos = 100, windows past the end, pos - 100 = n_frames), then
   * eegfx_process_recording (host and device buffers), both numerics,
   * eegfx_process_recording_epochs (epochs + features in one pass), both numerics,
-  * eegfx_extract_features_f64 on the oracle's epochs with a random feature size and skip.
+  * eegfx_extract_features_f64 on the oracle's epochs with a random feature size and skip,
+  * every fifth case, eegfx_process_recording_streamed with a random chunk size (EXACT).
 EXACT must equal the oracle value for value (epochs always); fma within 1e-9 per feature.
 
   python tools/parity_sweep.py [--cases 2000] [--seed0 0] [--out summary.json]
@@ -93,6 +94,12 @@ def main():
         ok, err2 = fma_ok(f, want)
         results.append(("process_recording_epochs fma",
                         ok and np.array_equal(ep, want_ep, equal_nan=True), err2))
+        if seed % 5 == 0:  # the streamed ingest (configs[4]) with a random chunk size
+            cf = int(np.random.default_rng(seed).integers(787, max(788, raw.shape[0] + 1)))
+            results.append(("process_recording_streamed exact",
+                            np.array_equal(ex.process_recording_streamed(raw, ct, cols, res, pos,
+                                                                         chunk_frames=cf),
+                                           want, equal_nan=True), 0.0))
         dep = torch.from_numpy(want_ep).cuda()
         got = ex.extract_features(dep, feature_size=nfeat, skip=skip)
         results.append(("extract_features exact device",
