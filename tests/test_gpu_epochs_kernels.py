@@ -60,11 +60,13 @@ def test_device_batch_extract_feature_size_and_skip(ctxs, nf, skip, C):
     assert np.max(np.abs(got_f - want)) <= 1e-9
 
 
-def test_device_batch_extract_zero_rows(ctxs):
-    """An all-zero window normalises to NaN (0/0), as SignalProcessing.normalize does."""
+@pytest.mark.parametrize("C", [3, 32])
+def test_device_batch_extract_zero_rows(ctxs, C):
+    """An all-zero window normalises to NaN (0/0), as SignalProcessing.normalize does (rows in LDS
+    at C = 3, rescaled in the output at C = 32)."""
     import torch
-    ep = np.zeros((9, 3, 750))
-    ep[3] = np.random.default_rng(5).standard_normal((3, 750))
+    ep = np.zeros((9, C, 750))
+    ep[3] = np.random.default_rng(5).standard_normal((C, 750))
     want = oracle.extract_features(ep)
     for c in ctxs:
         got = c.extract_features(torch.from_numpy(ep).cuda()).cpu().numpy()
