@@ -16,7 +16,8 @@ Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").  Extra legs:
                 the stream the kernel runs on, against 8.0 TB/s (MI355X_MICROARCH.md); traffic =
                 HBM bytes per launch from the committed rocprofv3 PMC summary (else null);
   cpu_baseline  the C restatement (oracle/, reference-faithful full pyramid) timed on the host
-                cores on a bounded sample of the same workload (rank 0, N=1 only).
+                cores on a bounded sample of the same workload (rank 0's shard; at N > 1 after
+                the gather legs).
 """
 import argparse
 import json
@@ -100,6 +101,12 @@ def parse():
                     help="untimed steps after the warmup for at least this much wall time, so the "
                          "timed steps start past the clock's power-cap transient (reported as "
                          "config.settle; DESIGN.md §7); 0 disables")
+    ap.add_argument("--plant", default=None, metavar="KIND:RATE",
+                    help="c3 study only (DESIGN.md §3.1): overwrite the spans [pos-100, pos+750) of "
+                         "a fraction RATE of the markers, evenly spread, with 'flat' (constant "
+                         "samples, the flat stretch of DoD2015_01: certified by the guard's second "
+                         "stage) or 'null' (a Nyquist-alternating +-1000-count signal on the DC "
+                         "level, in the filters' null space: recomputed under EXACT) windows")
     ap.add_argument("--trace-steps", action="store_true",
                     help="study only: device time of every warmup and timed step (HIP events "
                          "between steps), reported under 'step_trace'")
@@ -274,6 +281,7 @@ def main():
     pos = torch.arange(sp, sp * (n + 1), sp, dtype=torch.int64, device=dev)
     out = torch.empty((n, 16 * C), dtype=torch.float64, device=dev)
     cols, res = list(range(C)), [0.1] * C
+    planted = plant_windows(torch, raw, pos, args.plant) if args.plant else None
 
     def step():
         ctx.process_recording(raw, ct, cols, res, pos, out=out)
@@ -309,6 +317,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
 
+    ctx.guard_detail(reset=True)  # the guard counters then cover exactly the timed steps
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ctx.set_timing(True)  # HIP events around each window_kernel launch, on the context stream
@@ -328,7 +337,7 @@ def main():
         raise RuntimeError(f"timed {launches} window_kernel launches for {args.steps} steps")
     kernel_ms = win_total_ms / launches                 # average window_kernel launch duration
     kernel_bytes = win_bytes // launches                # algorithmic bytes per launch
-    guard_checked, guard_redone = ctx.guard_stats()     # warmup + timed steps (fma numerics)
+    guard_checked, guard_rechecked, guard_redone = ctx.guard_detail()  # the timed steps (fma)
 
     t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64, device=dev)
     if distributed:
@@ -393,7 +402,9 @@ def main():
                 "numerics": args.numerics,
                 "kernels": kernels,
                 "unit_rows_check": ok_norm,
-                "guard": guard_report(args, fx, dev, guard_checked, guard_redone),
+                "guard": guard_report(args, fx, dev, guard_checked, guard_rechecked,
+                                      guard_redone),
+                "planted": planted,
                 "settle": {"min_ms": args.settle_ms, "ms": round(settle_ms, 1),
                            "steps": settle_steps,
                            "note": "untimed steps between the warmup and the timed region, until "
@@ -450,9 +461,14 @@ def main():
             gather = {"op": None, "ms": None, "error": f"{type(exc).__name__}: {exc}"[:300]}
         watchdog.disarm()
 
+    # rank 0's host cores on a bounded sample of its own shard; at N > 1 after the gather legs,
+    # so the timed extraction and gathers ran with every rank's host threads quiet
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and args.cpu_sample > 0:
         cpu = cpu_baseline(args, raw, out, ct, C, sp)
+        if distributed:
+            cpu["sample"] += (f"; rank 0 of {world}, after the gather legs (the other ranks idle "
+                              "in teardown)")
 
     if rank == 0:
         line["cpu_baseline"] = cpu
@@ -466,20 +482,24 @@ def main():
         emit(line)
 
     if distributed:
-        watchdog.arm(60, None, "teardown")  # the line is out; do not hang in teardown
+        # the line is out; do not hang in teardown (rank 0 may still be timing the CPU baseline
+        # while the other ranks get here)
+        watchdog.arm(180 if rank else 60, None, "teardown")
     ctx.close()
     if distributed:
         dist.destroy_process_group()
     watchdog.disarm()
 
 
-def guard_report(args, fx, dev, checked, redone):
-    """The fma conditioning guard: rows of the timed run it could not certify and
-    sent to the EXACT follow-up launch, and the same rate on every marker of the reference's two
-    recordings (tests/golden/test-data, the repo's copies), outside the timed region."""
+def guard_report(args, fx, dev, checked, rechecked, redone):
+    """The fma conditioning guard over the timed steps: rows checked, rows that
+    failed the a-priori test and went to the second stage (the row's measured max |x|), rows that
+    failed that too and were recomputed under EXACT; and the same on every marker of the
+    reference's two recordings (tests/golden/test-data, the repo's copies), outside the timed
+    region."""
     if args.numerics != "fma":
         return None
-    rep = {"rows_checked": checked, "rows_recomputed": redone,
+    rep = {"rows_checked": checked, "rows_rechecked": rechecked, "rows_recomputed": redone,
            "rate": (redone / checked) if checked else None, "reference_recordings": {}}
     data = os.path.join(REPO, "tests", "golden", "test-data", "DoD")
     c = fx.Context(dev.index, numerics="fma")
@@ -488,15 +508,50 @@ def guard_report(args, fx, dev, checked, redone):
             base = os.path.join(data, stem)
             raw = fx.read_raw(base + ".vhdr", base + ".eeg")
             allpos = [m.position for m in fx.read_markers(base + ".vmrk") if m.position >= 100]
-            c.guard_stats(reset=True)
+            c.guard_detail(reset=True)
             c.process_recording(raw, raw.shape[1], [0, 1, 2], [0.1] * 3, allpos)
-            k, r = c.guard_stats()
-            rep["reference_recordings"][stem] = {"markers": k, "rows_recomputed": r}
+            k, rc, r = c.guard_detail()
+            rep["reference_recordings"][stem] = {"markers": k, "rows_rechecked": rc,
+                                                 "rows_recomputed": r}
     except Exception as exc:  # the recordings are test fixtures; report, do not fail the line
         rep["reference_recordings"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
     finally:
         c.close()
     return rep
+
+
+def plant_selection(n, rate):
+    """Indices of the markers --plant overwrites: round(rate * n) of them, evenly spread over
+    [0, n) (marker i when floor((i + 1) * rate) > floor(i * rate))."""
+    i = np.arange(n, dtype=np.float64)
+    return np.nonzero(np.floor((i + 1) * rate) > np.floor(i * rate))[0]
+
+
+def plant_windows(torch, raw, pos, spec, chunk=100_000):
+    """--plant KIND:RATE (study only): overwrite the frames [pos-100, pos+750) of the selected
+    markers, every channel, with 'flat' samples (the value at pos-100, held: the flat stretch of
+    DoD2015_01) or 'null' samples (DC + 1000 (-1)^f counts: a Nyquist-alternating window, which
+    the 12-decimal low-pass taps cancel to rounding level).  Markers are spaced >= 850 frames
+    apart, so the spans do not overlap."""
+    kind, _, rate = spec.partition(":")
+    rate = float(rate)
+    if kind not in ("flat", "null") or not 0.0 <= rate <= 1.0:
+        raise SystemExit("--plant KIND:RATE with KIND flat|null and 0 <= RATE <= 1")
+    sel = torch.from_numpy(plant_selection(pos.numel(), rate)).to(pos.device)
+    span = torch.arange(-100, 750, device=pos.device, dtype=torch.int64)
+    for a in range(0, sel.numel(), chunk):
+        p = pos[sel[a:a + chunk]]
+        idx = p[:, None] + span[None, :]                     # [m, 850] frames
+        if kind == "flat":
+            v = raw[p - 100][:, None, :].expand(-1, span.numel(), -1)
+        else:
+            sign = 1 - 2 * (idx & 1)
+            v = (-25000 + 1000 * sign)[:, :, None].expand(-1, -1, raw.shape[1])
+        raw[idx.reshape(-1)] = v.reshape(-1, raw.shape[1]).to(raw.dtype)
+    torch.cuda.synchronize(raw.device)
+    return {"kind": kind, "rate": rate, "markers": int(sel.numel()),
+            "note": "study workload, not the headline: the selected markers' spans overwritten "
+                    "on the device before the run"}
 
 
 class _Watchdog:

@@ -83,6 +83,8 @@ SIGNATURES = {
     "eegfx_ctx_set_numerics": (c_int, [c_void_p, c_int]),
     "eegfx_ctx_synchronize": (c_int, [c_void_p]),
     "eegfx_ctx_guard_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), c_int]),
+    "eegfx_ctx_guard_detail": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64),
+                                       POINTER(c_int64), c_int]),
     "eegfx_ctx_kernel_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double),
                                        POINTER(c_int64)]),
     "eegfx_ctx_set_timing": (c_int, [c_void_p, c_int]),

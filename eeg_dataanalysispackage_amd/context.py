@@ -149,6 +149,14 @@ class Context:
                                           1 if reset else 0))
         return int(a.value), int(b.value)
 
+    def guard_detail(self, reset: bool = False):
+        """(rows checked, rows that went to the guard's second stage, rows recomputed under EXACT)
+        since the context was created or last reset (eegfx_ctx_guard_detail; synchronises)."""
+        a, b, c = c_int64(), c_int64(), c_int64()
+        check(lib().eegfx_ctx_guard_detail(self.handle, ctypes.byref(a), ctypes.byref(b),
+                                           ctypes.byref(c), 1 if reset else 0))
+        return int(a.value), int(b.value), int(c.value)
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
             lib().eegfx_ctx_destroy(self._h)

@@ -149,9 +149,10 @@ struct eegfx_ctx {
   DevBuf raw, pos, out, scratch, fused;
   DevBuf lr_x, lr_y, lr_state, lr_part;  // logistic regression (eegfx_logreg_*)
   PinBuf pin_in, pin_out;                // small-batch extract_features staging (zero-copy)
-  // The fma numerics' conditioning guard (guard.h): a device word pair (the flagged-row count of
-  // the current launch, then the running total of recomputed rows) and the flagged-row list;
-  // guard_checked counts the rows that went through a guarded launch.
+  // The fma numerics' conditioning guard (guard.h): device words (the flagged-row count of the
+  // current window_wide_kernel launch; at +8 B the running total of recomputed rows; at +16 B the
+  // running total of rows that went to the second stage) and the flagged-row list; guard_checked
+  // counts the rows that went through a guarded launch.
   int* guard_dev = nullptr;
   DevBuf guard_list;
   int64_t guard_checked = 0;
@@ -159,7 +160,7 @@ struct eegfx_ctx {
     if (numerics == EEGFX_EXACT) return Guard{nullptr, nullptr, nullptr};
     guard_checked += n;
     return Guard{guard_dev, (int64_t*)guard_list.get(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1)),
-                 (unsigned long long*)(guard_dev + 2)};
+                 (unsigned long long*)(guard_dev + 2), (unsigned long long*)(guard_dev + 4)};
   }
   void bind_buffers() {
     for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
@@ -633,8 +634,8 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     HIP_CHECK(hipHostMalloc((void**)&c->err_host, sizeof(int), hipHostMallocMapped));
     *c->err_host = 0;
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
-    HIP_CHECK(hipMalloc((void**)&c->guard_dev, 16));
-    HIP_CHECK(hipMemset(c->guard_dev, 0, 16));
+    HIP_CHECK(hipMalloc((void**)&c->guard_dev, 24));
+    HIP_CHECK(hipMemset(c->guard_dev, 0, 24));
     *out = c.release();
   });
 }
@@ -685,23 +686,29 @@ int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
   });
 }
 
-int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_recomputed,
-                          int reset) {
+int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_rechecked,
+                           int64_t* rows_recomputed, int reset) {
   return guarded([&] {
     if (!ctx || !rows_checked || !rows_recomputed) fail(EEGFX_EINVAL, "null argument");
     ctx->activate();
-    unsigned long long total = 0;
-    HIP_CHECK(hipMemcpyAsync(&total, ctx->guard_dev + 2, sizeof(total), hipMemcpyDeviceToHost,
+    unsigned long long tot[2] = {0, 0};  // recomputed, rechecked
+    HIP_CHECK(hipMemcpyAsync(tot, ctx->guard_dev + 2, sizeof(tot), hipMemcpyDeviceToHost,
                              ctx->stream));
     ctx->drain();
     *rows_checked = ctx->guard_checked;
-    *rows_recomputed = (int64_t)total;
+    *rows_recomputed = (int64_t)tot[0];
+    if (rows_rechecked) *rows_rechecked = (int64_t)tot[1];
     if (reset) {
-      HIP_CHECK(hipMemsetAsync(ctx->guard_dev + 2, 0, sizeof(total), ctx->stream));
+      HIP_CHECK(hipMemsetAsync(ctx->guard_dev + 2, 0, sizeof(tot), ctx->stream));
       ctx->drain();
       ctx->guard_checked = 0;
     }
   });
+}
+
+int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_recomputed,
+                          int reset) {
+  return eegfx_ctx_guard_detail(ctx, rows_checked, nullptr, rows_recomputed, reset);
 }
 
 int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,

@@ -115,8 +115,24 @@ __device__ __forceinline__ const uint8_t* safe_quad(const uint8_t* raw, int64_t 
 #ifndef EEGFX_XCD_REMAP
 #define EEGFX_XCD_REMAP 1
 #endif
+// EEGFX_XCD_SUPER = T > 0: the grid is walked in rounds of 8T tiles, XCD x taking the T contiguous
+// tiles x*T .. x*T+T-1 of each round (the last, partial round as above), so the eight XCDs' read
+// streams stay within 8T tiles of each other however large the grid is.
+#ifndef EEGFX_XCD_SUPER
+#define EEGFX_XCD_SUPER 0
+#endif
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
   if (!EEGFX_XCD_REMAP) return b;
+  if (EEGFX_XCD_SUPER > 0) {
+    constexpr uint32_t T = EEGFX_XCD_SUPER > 0 ? EEGFX_XCD_SUPER : 1;
+    const uint32_t full = nb / (8 * T), k = b / 8;
+    if (k < full * T) return (k / T) * 8 * T + (b % 8) * T + k % T;
+    b -= full * 8 * T;  // b % 8 and b / 8 - full T as before: the remainder remapped alone
+    const uint32_t base = full * 8 * T;
+    nb -= base;
+    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+    return base + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+  }
   const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }

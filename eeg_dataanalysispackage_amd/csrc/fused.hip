@@ -393,7 +393,35 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
           },
           C, 16, fb + kSub * F, row, lane);
     };
-    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo);
+    // the guard's second stage: the row's measured max |x| per channel, from the staged window
+    // (epochs 1-7; epoch 0's window lies under the rows, so it is read from the recording)
+    auto recheck = [&](int e) {
+      const int64_t W = wb[e0 + e];
+      auto decode = [&](int c, float v) {
+        float y = v * sel.res[c];
+        y = y - base[(e0 + e) * C + c];
+        return (double)y;
+      };
+      if (e == 0) {  // uniform
+        const int64_t B = W & ~(int64_t)1;
+        const int64_t f0 = B / G::FB;
+        return guard_measured_x2_wave(
+            [&](int c, int k) -> float {
+              return f0 + k < n_frames
+                         ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
+                         : 0.0f;
+            },
+            decode, C, lane);
+      }
+      const uint8_t* ebe = (const uint8_t*)(win + e * G::ESTR) + ((uint32_t)W & 14u);
+      return guard_measured_x2_wave(
+          [&](int c, int k) -> float {
+            return (float)*(const int16_t*)(ebe + 16 * G::SEGQ * (k >> 6) + G::FB * (k & 63) +
+                                            2 * sel.col[c]);
+          },
+          decode, C, lane);
+    };
+    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo, recheck);
   }
 }
 

@@ -8,15 +8,22 @@
 // (SignalProcessing.java:38-52 divides by the norm), so a row is certified within 0.5e-9 (half of
 // the north_star's 1e-9; the normalisations' own rounding, ~1e-15, takes the rest) when
 //     |f_fma|^2 >= K2 * sum_c X_c^2,     K2 = (2 / 0.5e-9)^2 * 8 (E_a6^2 + E_d6^2) * 1.25.
-// A row that fails the test -- its features are close to rounding noise, e.g. a window in the
-// filters' null space (an alternating +-A signal) -- is appended to the guard list, and a
-// follow-up launch (guard.hip exact_rows_kernel) recomputes exactly those rows with the EXACT
-// filter bank, value-identical to the reference.
+// A row that fails the test -- its features are close to rounding noise, or X_c is loose -- goes
+// to a second stage: the wave that normalises it measures the row's own max |x| per channel
+// (guard_measured_x2_wave) and tests again with that X.  Only rows that still fail (e.g. a window
+// in the filters' null space, an alternating +-A signal) are recomputed with the EXACT filter bank,
+// value-identical to the reference, by the same wave inside the same kernel
+// (dwt8_exact_row_wave): the 3-channel window kernel, the 32-channel kernel, the one-pass kernels,
+// the batch extract and the per-epoch kernel.  Only the generic any-layout window kernel
+// (window_wide_kernel) appends its failing rows to `list` for a follow-up launch
+// (guard.hip exact_rows_kernel); `count` / `list` are unused elsewhere.
 //
 // X_c: for int16 recordings a bound known without touching the window,
 //   |x| = |fl(fl(raw * r) - b)| <= (32768 |r| + |b|)(1 + 2^-23) for every int16 raw (zero padding
-//   included), taken with a 2^-20 margin; for float32 recordings and caller-supplied double epochs
-//   the measured max |x| of the window (no a-priori bound exists).
+//   included), taken with a 2^-20 margin -- loose when the samples stay far below full scale (a
+//   flat stretch decodes to ~1e-3 against X ~ 6e3), hence the second stage; for float32 recordings
+//   and caller-supplied double epochs the measured max |x| of the window from the start (no
+//   a-priori bound exists).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,14 +37,16 @@ namespace eegfx {
 constexpr double kGuardK2Collapsed = 7.02e-05;
 constexpr double kGuardK2Cascade = 1.62e-04;
 
-// Device state of a guarded launch: `count` flagged rows so far (zeroed before the launch that
-// fills it), their epoch indices in `list` (capacity: the launch's epochs), and the running total
-// of recomputed rows since the context was created (eegfx_ctx_guard_stats).  count == nullptr
-// disables the guard (EXACT numerics).
+// Device state of a guarded launch: `count` flagged rows so far and their epoch indices in `list`
+// (window_wide_kernel only: zeroed before the launch that fills it, capacity the launch's epochs),
+// the running total of rows recomputed under EXACT since the context was created, and of rows that
+// failed the a-priori test and went to the second stage (`rechecked`; may be null)
+// (eegfx_ctx_guard_stats / eegfx_ctx_guard_detail).  total == nullptr disables the guard (EXACT).
 struct Guard {
   int* count;
   int64_t* list;
   unsigned long long* total;
+  unsigned long long* rechecked = nullptr;
 };
 
 namespace dev {
@@ -57,6 +66,51 @@ __device__ __forceinline__ void guard_flag(const Guard& g, int64_t e) {
 // sum of squares `acc` against the row's threshold; NaN fails (and is recomputed as EXACT).
 __device__ __forceinline__ bool guard_fails(double acc, double k2, double sum_x2) {
   return !(acc >= k2 * sum_x2);
+}
+
+__device__ __forceinline__ void guard_count_rechecked(const Guard& g, int rows) {
+  if (g.rechecked && rows) atomicAdd(g.rechecked, (unsigned long long)rows);
+}
+
+// The second stage, by one wave (every lane calls it; the result is wave-uniform): sum over the
+// row's C signals of X_c^2, X_c = max_k |x_c[k]| over the 512 window samples, measured.
+// sample(c, k) returns the raw value of sample k of channel c as a float (int16 values are exact;
+// 0 for the zero padding past the recording's end); the decode x = fl(fl(raw * r) - b) is monotone
+// in raw, so X_c = max(|x(min raw)|, |x(max raw)|) with decode(c, v) the kernels' own fp32 decode.
+// 16 lanes per channel, four channels per pass.  The 2^-20 margin covers the rounding of the sum.
+template <typename Sample, typename Decode>
+__device__ __forceinline__ double guard_measured_x2_wave(Sample sample, Decode decode, int C,
+                                                         int lane) {
+  const int grp = lane >> 4, l = lane & 15;
+  double sx = 0.0;
+#pragma unroll 1
+  for (int c0 = 0; c0 < C; c0 += 4) {
+    const int c = c0 + grp;
+    float lo = 0.0f, hi = 0.0f;
+    if (c < C) {
+      lo = hi = sample(c, l);
+#pragma unroll 4
+      for (int k = l + 16; k < 512; k += 16) {
+        const float v = sample(c, k);
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+      }
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      lo = fminf(lo, __shfl_xor(lo, off, 64));
+      hi = fmaxf(hi, __shfl_xor(hi, off, 64));
+    }
+    double x2 = 0.0;
+    if (c < C) {
+      const double X = fmax(fabs(decode(c, lo)), fabs(decode(c, hi)));
+      x2 = X * X;
+    }
+    x2 += __shfl_xor(x2, 16, 64);
+    x2 += __shfl_xor(x2, 32, 64);
+    sx += x2;
+  }
+  return sx * (1.0 + 0x1p-20);
 }
 
 }  // namespace dev

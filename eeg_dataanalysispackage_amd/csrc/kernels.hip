@@ -207,9 +207,22 @@ __device__ __forceinline__ void staged_features(Smp smp, GSmp gsmp, const int* s
         acc += __shfl_xor(acc, off, 64);
         sx += __shfl_xor(sx, off, 64);
       }
+      bool fails = guard.total && guard_fails(acc, kGuardK2Collapsed, sx);  // wave-uniform
+      if (!MEASURE && fails) {  // int16: the second stage, the row's measured max |x|
+        if (lane == 0) guard_count_rechecked(guard, 1);
+        fails = guard_fails(acc, kGuardK2Collapsed,
+                            guard_measured_x2_wave(
+                                [&](int c, int k) { return gsmp(175 + k, s_col[c]); },
+                                [&](int c, float v) {
+                                  float y = v * s_res[c];
+                                  y = y - s_base[c];
+                                  return (double)y;
+                                },
+                                C, lane));
+      }
       if (lane == 0) {
         sh[0] = rsqrt_nr(acc);
-        sh[1] = guard.total && guard_fails(acc, kGuardK2Collapsed, sx) ? 1.0 : 0.0;
+        sh[1] = fails ? 1.0 : 0.0;
       }
     } else if (lane == 0) {
       double acc = 0.0;
@@ -393,7 +406,21 @@ __global__ __launch_bounds__(256) void cut_features_c3_kernel(
           },
           C, 16, fb + kCfEpochs * F, row, lane);
     };
-    normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo);
+    // the guard's second stage: the row's measured max |x| per channel, from the recording
+    auto recheck = [&](int e) {
+      const int64_t f0 = sP[e] + 175;
+      return guard_measured_x2_wave(
+          [&](int cc, int k) -> float {
+            return f0 + k < n_frames ? (float)raw[(f0 + k) * CT + s_col[cc]] : 0.0f;
+          },
+          [&](int cc, float v) {
+            float y = v * s_res[cc];
+            y = y - s_base[e * C + cc];
+            return (double)y;
+          },
+          C, lane);
+    };
+    normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo, recheck);
   }
 }
 

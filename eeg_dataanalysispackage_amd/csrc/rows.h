@@ -23,16 +23,22 @@ namespace dev {
 //          back to LDS and leave as contiguous non-temporal 1 KB wave stores (storing each lane's
 //          16-byte pieces 48 B apart cost 1,114 instead of 384 written bytes per row).  A row
 //          whose sum of squares fails the conditioning guard (guard.h; gx = the C per-signal X^2)
-//          is recomputed under EXACT by redo(e, row) into its row slot before the store (rare:
-//          never on the bench workload), and counted in the guard's running total.
+//          goes to the second stage: recheck(e), a wave-collective call, returns the row's
+//          measured sum of X_c^2, and only rows that fail again are recomputed under EXACT by
+//          redo(e, row) into their row slots before the store (rare: never on the bench workload),
+//          and counted in the guard's running total.  Every recheck runs before the first redo,
+//          whose LDS scratch may overwrite the staged windows that a recheck reads.
 struct NoRedo {
   __device__ void operator()(int, double*) const {}
 };
-template <int F, bool FAST, int C = F / 16, typename Redo = NoRedo>
+struct NoRecheck {  // no second stage: every flagged row is recomputed
+  __device__ double operator()(int) const { return __builtin_inf(); }
+};
+template <int F, bool FAST, int C = F / 16, typename Redo = NoRedo, typename Recheck = NoRecheck>
 __device__ __forceinline__ void normalise_store(double* fb, double* norm, double* o, int ne,
                                                 int lane, const double* gx = nullptr,
                                                 Guard g = Guard{nullptr, nullptr, nullptr},
-                                                Redo redo = Redo{}) {
+                                                Redo redo = Redo{}, Recheck recheck = Recheck{}) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   if constexpr (FAST) {
     static_assert(F % 16 == 0, "8 lanes per row, pairs of features");
@@ -62,14 +68,22 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
         *(double2*)(fb + e * F + p * P + i) = make_double2(v[i] * inv, v[i + 1] * inv);
     }
     wave_sync();
-    uint64_t flagged = __ballot(fails);  // bit 8e: row e failed the guard
+    uint64_t flagged = __ballot(fails);  // bit 8e: row e failed the a-priori test
     if (flagged) {                        // uniform, rare
-      if (lane == 0) atomicAdd(g.total, (unsigned long long)__popcll(flagged));
-      do {
-        const int e1 = __ffsll((unsigned long long)flagged) - 1;
+      uint64_t left = 0;                  // rows that fail the measured test too
+      for (uint64_t f = flagged; f; f &= f - 1) {
+        const int e1 = __ffsll((unsigned long long)f) - 1;
+        const double acc_e = __shfl(acc, e1, 64);
+        if (guard_fails(acc_e, kGuardK2Collapsed, recheck(e1 >> 3))) left |= 1ull << e1;
+      }
+      if (lane == 0) {
+        guard_count_rechecked(g, __popcll(flagged));
+        if (left) atomicAdd(g.total, (unsigned long long)__popcll(left));
+      }
+      for (; left; left &= left - 1) {
+        const int e1 = __ffsll((unsigned long long)left) - 1;
         redo(e1 >> 3, fb + (e1 >> 3) * F);
-        flagged &= flagged - 1;
-      } while (flagged);
+      }
     }
     for (int i = 2 * lane; i < ne * F; i += 128)
       __builtin_nontemporal_store(*(const f64x2*)(fb + i), (f64x2*)(o + i));

@@ -251,9 +251,28 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
         acc += __shfl_xor(acc, off, 64);
         sx += __shfl_xor(sx, off, 64);
       }
+      bool fails = guard.count && guard_fails(acc, kGuardK2Collapsed, sx);  // wave-uniform
+      if (std::is_same<T, int16_t>::value && fails) {  // the second stage on the staged window
+        if (lane == 0) guard_count_rechecked(guard, 1);
+        const int64_t B = (wpos(m) + 175) * FB;
+        const uint8_t* eb = win + (size_t)m * EQ * 16 + (int)(B & 15);
+        fails = guard_fails(
+            acc, kGuardK2Collapsed,
+            guard_measured_x2_wave(
+                [&](int c, int k) -> float {
+                  return sample_at<T>(eb + sel.col[c] * (int)sizeof(T) + 16 * SEGQ * (k >> 6) +
+                                      FB * (k & 63));
+                },
+                [&](int c, float v) {
+                  float y = v * sel.res[c];
+                  y = y - base[(e0 + m) * C + c];
+                  return (double)y;
+                },
+                C, lane));
+      }
       if (lane == 0) {
         norm[m] = rsqrt_nr(acc);  // the reciprocal norm (multiplied below)
-        if (guard.count && guard_fails(acc, kGuardK2Collapsed, sx)) guard_flag(guard, e0 + m);
+        if (fails) guard_flag(guard, e0 + m);
       }
     }
   } else {
@@ -377,9 +396,26 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
         acc += __shfl_xor(acc, off, 64);
         sx += __shfl_xor(sx, off, 64);
       }
+      bool fails = EEGFX_GUARD && guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
+      if (fails) {  // wave-uniform, rare: the second stage on the staged window (still intact)
+        if (lane == 0) guard_count_rechecked(guard, 1);
+        fails = guard_fails(
+            acc, kGuardK2Collapsed,
+            guard_measured_x2_wave(
+                [&](int cc, int k) -> float {
+                  return (float)sample_at<int16_t>(win + (int)(B & 15) + sel.col[cc] * 2 +
+                                                   16 * SEGQ * (k >> 6) + FB * (k & 63));
+                },
+                [&](int cc, float v) {
+                  float y = v * sel.res[cc];
+                  y = y - base[e * C + cc];
+                  return (double)y;
+                },
+                C, lane));
+      }
       if (lane == 0) {
         norm1 = rsqrt_nr(acc);
-        redo = EEGFX_GUARD && guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
+        redo = fails;
       }
     }
     __syncthreads();

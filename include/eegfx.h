@@ -25,7 +25,7 @@
  * validated by the kernels that read them (OffLineDataProvider.java:220-225: pos-100 must lie
  * in [0, n_frames]); a violation is reported as EEGFX_ERANGE by the next call on that context
  * that synchronises it, which also clears it.  The calls that synchronise are
- * eegfx_ctx_synchronize, eegfx_ctx_guard_stats, every EEGFX_MEM_HOST compute call,
+ * eegfx_ctx_synchronize, eegfx_ctx_guard_stats / _detail, every EEGFX_MEM_HOST compute call,
  * eegfx_read_raw with EEGFX_MEM_DEVICE, eegfx_logreg_sgd_train / eegfx_svm_sgd_train, and
  * eegfx_logreg_predict / eegfx_svm_predict with EEGFX_MEM_DEVICE.  When such a call returns
  * EEGFX_ERANGE for an earlier call's position, its own work has completed and its outputs are
@@ -111,9 +111,17 @@ int eegfx_ctx_kernel_stats(eegfx_ctx* ctx, int64_t* launches, double* total_ms,
                            int64_t* total_bytes);
 /* The fma numerics' conditioning guard: rows that went through a guarded (EEGFX_FMA) feature
  * launch on this context, and rows the guard recomputed under EEGFX_EXACT, since the context was
- * created or last reset (reset != 0 clears both after reading).  Synchronises the context. */
+ * created or last reset (reset != 0 clears both after reading).  Synchronises the context.
+ * Guarded launches include the feature rows eegfx_odp_load_data computes for the provider's
+ * resident feature matrix (eegfx_odp_get_features copies them), on the context it was given. */
 int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_recomputed,
                           int reset);
+/* The same counters, with the rows that failed the guard's a-priori test and went to its second
+ * stage (the row's measured max |x|): rows_rechecked >= rows_recomputed, and
+ * rows_rechecked - rows_recomputed rows were certified by the second stage.  rows_rechecked may be
+ * NULL. */
+int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_rechecked,
+                           int64_t* rows_recomputed, int reset);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
 /* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */

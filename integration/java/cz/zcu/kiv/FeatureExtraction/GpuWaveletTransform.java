@@ -1,0 +1,89 @@
+package cz.zcu.kiv.FeatureExtraction;
+
+/**
+ * fe=dwt-8 on an MI355X through libeegfx: a drop-in for WaveletTransform(8, 512, 175, 16)
+ * (WaveletTransform.java:82-141) behind IFeatureExtraction (IFeatureExtraction.java:27-35).
+ * Registered next to the CPU extractor in PipelineBuilder.java:127-139:
+ *     case "dwt-8-gpu": fe = new GpuWaveletTransform(8, 512, 175, 16); break;
+ * Java 7/8 (Spark 1.6); natives in integration/jni/eegfx_jni.c (libeegfx_jni.so).
+ */
+public class GpuWaveletTransform implements IFeatureExtraction {
+    static { System.loadLibrary("eegfx_jni"); }
+
+    /** Channels the reference extracts (WaveletTransform.CHANNELS = {1, 2, 3}: Fz, Cz, Pz). */
+    private static final int CHANNELS = 3;
+    private static final int POSTSTIMULUS = 750;   // Const.POSTSTIMULUS_VALUES
+
+    // One device context per calling thread: extractFeatures is reached concurrently from the
+    // Spark local[*] executor threads (LogisticRegressionClassifier.java:50,90), and an eegfx
+    // context drives one stream.
+    private static final ThreadLocal<Long> CTX = new ThreadLocal<Long>() {
+        @Override protected Long initialValue() {
+            long c = nativeCreate(0);
+            if (c == 0) throw new IllegalStateException(nativeLastError());
+            return c;
+        }
+    };
+
+    private int name, epochSize, skipSamples, featureSize;
+
+    public GpuWaveletTransform() { this(8, 512, 175, 16); }
+
+    public GpuWaveletTransform(int name, int epochSize, int skipSamples, int featureSize) {
+        setWaveletName(name);
+        setEpochSize(epochSize);
+        setSkipSamples(skipSamples);
+        setFeatureSize(featureSize);
+    }
+
+    @Override
+    public double[] extractFeatures(double[][] epoch) {
+        return extractFeaturesBatch(new double[][][] { epoch })[0];
+    }
+
+    /** The batched form: one call per Spark partition (mapPartitions) instead of one per epoch. */
+    public double[][] extractFeaturesBatch(double[][][] epochs) {
+        int n = epochs.length;
+        double[] flat = new double[n * CHANNELS * POSTSTIMULUS];
+        for (int i = 0; i < n; i++)
+            for (int c = 0; c < CHANNELS; c++)
+                System.arraycopy(epochs[i][c], 0, flat, (i * CHANNELS + c) * POSTSTIMULUS, POSTSTIMULUS);
+        double[] out = new double[n * CHANNELS * featureSize];
+        int rc = nativeExtract(CTX.get(), flat, n, CHANNELS, name, epochSize, skipSamples,
+                               featureSize, out);
+        if (rc != 0) throw new IllegalArgumentException(nativeLastError());
+        double[][] rows = new double[n][CHANNELS * featureSize];
+        for (int i = 0; i < n; i++)
+            System.arraycopy(out, i * CHANNELS * featureSize, rows[i], 0, CHANNELS * featureSize);
+        return rows;
+    }
+
+    @Override
+    public int getFeatureDimension() { return featureSize * CHANNELS; }
+
+    // The reference's setters and their argument checks (WaveletTransform.java:160-215)
+    public void setWaveletName(int name) {
+        if (name < 0 || name > 17) throw new IllegalArgumentException("Wavelet Name must be >= 0 and <= 17");
+        this.name = name;
+    }
+
+    public void setEpochSize(int epochSize) {
+        if (epochSize > 0 && epochSize <= POSTSTIMULUS) this.epochSize = epochSize;
+        else throw new IllegalArgumentException("Epoch Size must be > 0 and <= " + POSTSTIMULUS);
+    }
+
+    public void setSkipSamples(int skipSamples) {
+        if (skipSamples > 0 && skipSamples <= POSTSTIMULUS) this.skipSamples = skipSamples;
+        else throw new IllegalArgumentException("Skip Samples must be > 0 and <= " + POSTSTIMULUS);
+    }
+
+    public void setFeatureSize(int featureSize) {
+        if (featureSize > 0 && featureSize <= 1024) this.featureSize = featureSize;
+        else throw new IllegalArgumentException("Feature Size must be > 0 and <= 1024");
+    }
+
+    private static native long nativeCreate(int device);
+    private static native int nativeExtract(long ctx, double[] epochs, int n, int C, int name,
+                                            int epochSize, int skip, int featureSize, double[] out);
+    private static native String nativeLastError();
+}

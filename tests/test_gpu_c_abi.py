@@ -5,8 +5,10 @@ import subprocess
 
 import pytest
 
-from conftest import DOD01
-from test_library_abi import _build_c_consumer
+import numpy as np
+
+from conftest import DOD01, INFO_TRAIN, hexrows
+from test_library_abi import _build_c_consumer, _build_shim_consumer
 
 pytestmark = pytest.mark.gpu
 
@@ -16,3 +18,32 @@ def test_plain_c_consumer_gpu(tmp_path):
     r = subprocess.run([exe, DOD01, "gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "golden sum matches" in r.stdout
+
+
+def test_java_shim_sequence_gpu(tmp_path, golden_vectors):
+    """The Java drop-in's exact call sequence through the JNI shim's core, from C
+    (tests/c_abi/shim_consumer.c): GpuOffLineDataProvider(infoTrain.txt) -> loadData ->
+    getData / getDataLabels / getFeatures, GpuWaveletTransform.extractFeatures one epoch per call
+    from four threads with a context each (equal to getFeatures bit for bit, checked in C) and
+    extractFeaturesBatch, GpuLogisticRegressionClassifier.train/test.  The rows must equal
+    golden_vectors.json's hex rows (EXACT numerics, the default) and the weights the MLlib
+    restatement's (parity unpinned: no reference fixture holds weights)."""
+    from oracle import mllib_logreg
+    exe = _build_shim_consumer(tmp_path)
+    r = subprocess.run([exe, INFO_TRAIN, "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "shim_consumer ok (gpu)" in r.stdout
+    lines = r.stdout.splitlines()
+    rows = [[float.fromhex(v) for v in l.split(":")[1].split()] for l in lines
+            if l.startswith("row ")]
+    want = hexrows(golden_vectors["infoTrain"]["features_hex"])
+    assert np.array_equal(np.array(rows), want)
+    w = np.array([float.fromhex(v) for v in
+                  next(l for l in lines if l.startswith("weights:")).split(":")[1].split()])
+    labels = np.array(golden_vectors["infoTrain"]["labels"], dtype=np.float64)
+    w_ref, _ = mllib_logreg.sgd_train(want, labels, 100, 1.0, 0.01)
+    assert np.linalg.norm(w - w_ref) <= 1e-9 * np.linalg.norm(w_ref)   # test_gpu_logreg.py's bound
+    stats = [int(v) for v in next(l for l in lines if l.startswith("statistics:")).split()[1:]]
+    pred = mllib_logreg.predict(want, w_ref)
+    from eeg_dataanalysispackage_amd.classification import reference_statistics
+    assert tuple(stats) == reference_statistics(pred, labels).as_tuple()

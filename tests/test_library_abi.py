@@ -90,6 +90,30 @@ def _build_c_consumer(tmp_path):
     return exe
 
 
+def _build_shim_consumer(tmp_path):
+    """tests/c_abi/shim_consumer.c + the JNI shim's core (integration/jni/eegfx_shim.c), plain C."""
+    exe = str(tmp_path / "shim_consumer")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    jni = os.path.join(REPO, "integration", "jni")
+    subprocess.run(["gcc", "-std=c99", "-O1", "-Wall", "-Werror", "-pthread",
+                    "-I", os.path.join(REPO, "include"), "-I", jni,
+                    os.path.join(REPO, "tests", "c_abi", "shim_consumer.c"),
+                    os.path.join(jni, "eegfx_shim.c"), "-L", libdir, "-leegfx",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    return exe
+
+
+def test_java_shim_core_host(tmp_path):
+    """The Java drop-in's shim core from C without a device: exception mapping, the reference's
+    confusion-matrix reading, and the planning-only provider on infoTrain.txt (11 epochs, 5
+    targets, OfflineDataProviderTest.java:65-88)."""
+    from conftest import INFO_TRAIN
+    exe = _build_shim_consumer(tmp_path)
+    r = subprocess.run([exe, INFO_TRAIN], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "shim_consumer ok (host)" in r.stdout
+
+
 def test_plain_c_consumer(tmp_path):
     """The ABI from plain C (what the JNI shim is): header parsing, marker planning against the
     reference golden, error statuses -- no GPU needed."""

@@ -5,6 +5,7 @@
 //   hipcc ... -DFUSED_SRC='"build/v1/fused.hip"' window_probe.hip -o window_probe_v1
 //   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
 //   PROBE_BASELINE=1: time the baseline kernel alone; PROBE_STEP=1: baseline + window per launch
+//   PROBE_N=8000000: another epoch count (one marker every 1,000 frames as always)
 //
 // Phase timestamps (per-workgroup s_memrealtime at each phase boundary):
 //   restore_variant.sh phase_timestamps_fused, then -DFUSED_SRC='"<dir>/fused.hip"' -DPROBE_TIMESTAMPS
@@ -36,7 +37,8 @@ int main() {
   const bool wide = getenv("PROBE_WIDE") != nullptr;
   const bool fast = getenv("PROBE_EXACT") == nullptr;
   const int ct = wide ? 32 : 3;
-  const int64_t n = wide ? 250000 : 1000000, nf = 1000 * n + 2000;
+  const char* en = getenv("PROBE_N");  // epochs (configs[2]'s rank shard: 8000000)
+  const int64_t n = en ? atoll(en) : wide ? 250000 : 1000000, nf = 1000 * n + 2000;
   int16_t* raw;
   int64_t* pos;
   float* base;
@@ -80,7 +82,9 @@ int main() {
     else if (time_baseline) baseline();
     else window();
   };
-  for (int r = 0; r < 200; ++r) one();
+  const char* wu = getenv("PROBE_WARMUP");
+  const int warm = wu ? atoi(wu) : 200;
+  for (int r = 0; r < warm; ++r) one();
   (void)hipEventRecord(a);
   for (int r = 0; r < iters; ++r) one();
   (void)hipEventRecord(b);
