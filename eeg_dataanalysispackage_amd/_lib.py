@@ -108,6 +108,11 @@ SIGNATURES = {
     "eegfx_logreg_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                        c_double, c_double, c_double, c_double, c_void_p,
                                        POINTER(c_int32), c_int]),
+    "eegfx_logreg_sgd_train_partitioned": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                                   c_int32, c_double, c_double, c_double, c_double,
+                                                   c_int32, c_void_p, POINTER(c_int32), c_int]),
+    "eegfx_spark_sample": (c_int, [c_int64, c_double, c_int32, c_int64, c_void_p,
+                                   POINTER(c_int64)]),
     "eegfx_logreg_predict": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_double,
                                      c_double, c_void_p, c_int]),
     "eegfx_svm_sgd_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,

@@ -14,7 +14,7 @@ Model save/load (Spark model directories) is out of scope.
 from __future__ import annotations
 
 import math
-from ctypes import byref, c_int32
+from ctypes import byref, c_int32, c_int64
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -31,7 +31,7 @@ CONVERGENCE_TOL = 0.001
 
 
 def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini_batch_fraction,
-           convergence_tol, initial_weights):
+           convergence_tol, initial_weights, num_partitions=None):
     if _is_device(X) != _is_device(y):
         raise ValueError("X and y must both be host or both be device arrays")
     X = _contig(X, np.float64)
@@ -44,9 +44,13 @@ def _train(entry, ctx: Context, X, y, num_iterations, step_size, reg_param, mini
     it = c_int32()
     mem = _mem(X, y)
     # ordered after the torch work that produced X / y (Context._call), like every device call
-    ctx._call(mem, X, getattr(lib(), entry), ctx.handle, ptr(X), ptr(y), n, d,
-              int(num_iterations), float(step_size), float(reg_param),
-              float(mini_batch_fraction), float(convergence_tol), ptr(w), byref(it), mem)
+    head = (ctx.handle, ptr(X), ptr(y), n, d, int(num_iterations), float(step_size),
+            float(reg_param), float(mini_batch_fraction), float(convergence_tol))
+    if num_partitions is None:
+        ctx._call(mem, X, getattr(lib(), entry), *head, ptr(w), byref(it), mem)
+    else:
+        ctx._call(mem, X, getattr(lib(), entry + "_partitioned"), *head, int(num_partitions),
+                  ptr(w), byref(it), mem)
     return w, it.value
 
 
@@ -69,11 +73,29 @@ def _predict(entry, ctx: Context, X, weights, intercept, threshold):
 def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
               step_size: float = DEFAULT_STEP_SIZE, reg_param: float = 0.0,
               mini_batch_fraction: float = DEFAULT_MINI_BATCH_FRACTION,
-              convergence_tol: float = CONVERGENCE_TOL, initial_weights=None):
-    """Full-batch LogisticRegressionWithSGD on the device; returns (weights, iterations_run).
-    X (n x d float64, host numpy or device torch) and y (n labels 0/1) may live on either side."""
+              convergence_tol: float = CONVERGENCE_TOL, initial_weights=None,
+              num_partitions: Optional[int] = None):
+    """LogisticRegressionWithSGD on the device; returns (weights, iterations_run).  X (n x d
+    float64, host numpy or device torch) and y (n labels 0/1) may live on either side.
+    mini_batch_fraction < 1 samples iteration i's mini-batch as MLlib's data.sample(false, f,
+    42 + i) over num_partitions Spark partitions (None: the host's hardware threads, Spark
+    local[*]; eegfx_logreg_sgd_train_partitioned)."""
     return _train("eegfx_logreg_sgd_train", ctx, X, y, num_iterations, step_size, reg_param,
-                  mini_batch_fraction, convergence_tol, initial_weights)
+                  mini_batch_fraction, convergence_tol, initial_weights, num_partitions)
+
+
+def spark_sample(n: int, fraction: float, num_partitions: int, seed: int) -> np.ndarray:
+    """RDD.sample(false, fraction, seed) of n rows in num_partitions slices (eegfx_spark_sample,
+    host only): the kept row indices, ascending."""
+    words = np.zeros((n + 31) // 32, dtype=np.uint32)
+    kept = c_int64()
+    from ._lib import check
+    check(lib().eegfx_spark_sample(int(n), float(fraction), int(num_partitions), int(seed),
+                                   ptr(words), byref(kept)))
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n]
+    rows = np.nonzero(bits)[0]
+    assert rows.size == kept.value
+    return rows
 
 
 def predict(ctx: Context, X, weights, intercept: float = 0.0,
@@ -157,6 +179,8 @@ class LogisticRegressionClassifier:
         self.config: Dict[str, str] = {}
         self.weights: Optional[np.ndarray] = None
         self.iterations_run = 0
+        # Spark partitions of the training RDD (mini-batch sampling only); None = local[*]
+        self.num_partitions: Optional[int] = None
 
     @property
     def context(self) -> Context:
@@ -191,7 +215,8 @@ class LogisticRegressionClassifier:
             self.weights, self.iterations_run = sgd_train(
                 self.context, X, y, num_iterations=int(c["config_num_iterations"]),
                 step_size=float(c["config_step_size"]), reg_param=0.0,
-                mini_batch_fraction=float(c["config_mini_batch_fraction"]))
+                mini_batch_fraction=float(c["config_mini_batch_fraction"]),
+                num_partitions=self.num_partitions)
         else:
             self.weights, self.iterations_run = sgd_train(
                 self.context, X, y, DEFAULT_NUM_ITERATIONS, DEFAULT_STEP_SIZE, DEFAULT_REG_PARAM,
@@ -240,4 +265,4 @@ class SVMClassifier(LogisticRegressionClassifier):
 
 
 __all__ = ["ClassificationStatistics", "LogisticRegressionClassifier", "SVMClassifier", "predict",
-           "reference_statistics", "sgd_train", "svm_predict", "svm_sgd_train", "EegfxError"]
+           "reference_statistics", "sgd_train", "spark_sample", "svm_predict", "svm_sgd_train", "EegfxError"]

@@ -20,6 +20,7 @@
 #include "common.h"
 #include "eegfx_ext.h"
 #include "launch.h"
+#include "spark_sample.h"
 
 using namespace eegfx;
 
@@ -147,7 +148,7 @@ struct eegfx_ctx {
   std::vector<int64_t> event_bytes;
   size_t n_timed = 0;
   DevBuf raw, pos, out, scratch, fused;
-  DevBuf lr_x, lr_y, lr_state, lr_part;  // logistic regression (eegfx_logreg_*)
+  DevBuf lr_x, lr_y, lr_state, lr_part, lr_mask;  // logistic regression (eegfx_logreg_*)
   PinBuf pin_in, pin_out;                // small-batch extract_features staging (zero-copy)
   // The fma numerics' conditioning guard (guard.h): device words (the flagged-row count of the
   // current window_wide_kernel launch; at +8 B the running total of recomputed rows; at +16 B the
@@ -164,12 +165,12 @@ struct eegfx_ctx {
   }
   void bind_buffers() {
     for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
-                      &guard_list})
+                      &lr_mask, &guard_list})
       b->sp = &stream;
   }
   void release_buffers() {
     for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
-                      &guard_list})
+                      &lr_mask, &guard_list})
       b->release();
     pin_in.release();
     pin_out.release();
@@ -1081,13 +1082,16 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
 }
 
 // the classifier of LogisticRegressionClassifier.java:85-114 on the GPU
-// (csrc/logreg.hip): MLlib 1.6.2 LogisticRegressionWithSGD, full batch.  miniBatchFraction < 1
-// samples each partition with Spark's own seeded Bernoulli sampler, which depends on Spark's
-// partitioning -- not reproducible outside Spark, so it is refused.
+// (csrc/logreg.hip): MLlib 1.6.2 LogisticRegressionWithSGD.  miniBatchFraction < 1: iteration i
+// trains on data.sample(false, f, 42 + i) of the rows in `num_partitions` ParallelCollectionRDD
+// slices (spark_sample.h), drawn on the host (threads over iterations) as one bit mask per
+// iteration and uploaded before the iterations that read them.  The hinge loop of
+// eegfx_ext.h (SVMWithSGD) stays full-batch (outside the contract, not extended).
 static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double* y, int64_t n,
                          int32_t d, int32_t num_iterations, double step_size, double reg_param,
-                         double mini_batch_fraction, double convergence_tol, double* weights,
-                         int32_t* iterations_run, int mem) {
+                         double mini_batch_fraction, double convergence_tol,
+                         int32_t num_partitions, double* weights, int32_t* iterations_run,
+                         int mem) {
   return guarded([&] {
     if (!ctx || !weights) fail(EEGFX_EINVAL, "null argument");
     check_mem(mem);
@@ -1095,9 +1099,14 @@ static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double
     if (!X || !y) fail(EEGFX_EINVAL, "null X / y");
     if (d < 1 || d > kLrMaxFeatures) fail(EEGFX_EINVAL, "d=%d outside [1, %d]", d, kLrMaxFeatures);
     if (num_iterations < 0) fail(EEGFX_EINVAL, "num_iterations %d", num_iterations);
-    if (mini_batch_fraction != 1.0)
-      fail(EEGFX_ENOTSUP, "miniBatchFraction %g: only full-batch (1.0) gradient descent",
+    // BernoulliSampler's require: f in [0, 1] up to RandomSampler.roundingEpsilon
+    if (!(mini_batch_fraction >= -1e-6 && mini_batch_fraction <= 1.0 + 1e-6))
+      fail(EEGFX_EINVAL, "Sampling fraction (%g) must be on interval [0, 1]", mini_batch_fraction);
+    const bool sampled = mini_batch_fraction < 1.0;
+    if (sampled && grad != kGradLogistic)
+      fail(EEGFX_ENOTSUP, "miniBatchFraction %g: the SVM loop is full-batch only",
            mini_batch_fraction);
+    if (sampled && num_partitions < 1) fail(EEGFX_EINVAL, "num_partitions %d", num_partitions);
     ctx->activate();
     const double* dX = X;
     const double* dy = y;
@@ -1121,9 +1130,39 @@ static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double
     HIP_CHECK(launch_lr_validate(ctx->stream, dy, n, st));
     const int G = lr_grid(n);
     double* part = (double*)ctx->lr_part.get(sizeof(double) * (size_t)G * d);
-    for (int i = 0; i < num_iterations; ++i)
-      HIP_CHECK(launch_lr_iteration(ctx->stream, grad, dX, dy, n, d, st, part, G, step_size,
-                                    reg_param, convergence_tol, num_iterations));
+    if (!sampled) {
+      for (int i = 0; i < num_iterations; ++i)
+        HIP_CHECK(launch_lr_iteration(ctx->stream, grad, dX, dy, n, d, nullptr, n, st, part, G,
+                                      step_size, reg_param, convergence_tol, num_iterations));
+    } else {
+      // the masks of up to ~256 MB of iterations at a time, drawn by threads over iterations
+      const int64_t words = (n + 31) / 32;
+      const int chunk = (int)std::max<int64_t>(
+          1, std::min<int64_t>(num_iterations, ((int64_t)64 << 20) / words));
+      std::vector<uint32_t> masks((size_t)(chunk * words));
+      std::vector<int64_t> counts((size_t)chunk);
+      uint32_t* dmask = (uint32_t*)ctx->lr_mask.get(sizeof(uint32_t) * masks.size());
+      for (int i0 = 0; i0 < num_iterations; i0 += chunk) {
+        const int k = std::min(chunk, num_iterations - i0);
+        ctx->drain();  // the previous chunk's upload and iterations are done with both buffers
+        const int T = (int)std::max<unsigned>(1, std::min<unsigned>(
+            (unsigned)k, std::min(64u, std::thread::hardware_concurrency())));
+        std::vector<std::thread> pool;
+        for (int t = 0; t < T; ++t)
+          pool.emplace_back([&, t] {
+            for (int j = t; j < k; j += T)  // GradientDescent's i = i0 + j + 1, seed 42 + i
+              counts[j] = spark::sample_mask(n, mini_batch_fraction, num_partitions,
+                                             42 + (int64_t)(i0 + j + 1), &masks[(size_t)j * words]);
+          });
+        for (auto& th : pool) th.join();
+        HIP_CHECK(hipMemcpyAsync(dmask, masks.data(), sizeof(uint32_t) * (size_t)(k * words),
+                                 hipMemcpyHostToDevice, ctx->stream));
+        for (int j = 0; j < k; ++j)
+          HIP_CHECK(launch_lr_iteration(ctx->stream, grad, dX, dy, n, d, dmask + (size_t)j * words,
+                                        counts[j], st, part, G, step_size, reg_param,
+                                        convergence_tol, num_iterations));
+      }
+    }
     HIP_CHECK(hipMemcpyAsync(hs.data(), st, sbytes, hipMemcpyDeviceToHost, ctx->stream));
     ctx->drain();
     if (h->converged == 2) fail(EEGFX_EINVAL, "Input validation failed: labels must be 0.0 or 1.0");
@@ -1165,12 +1204,35 @@ static int glm_predict(int grad, eegfx_ctx* ctx, const double* X, int64_t n, int
   });
 }
 
+int eegfx_logreg_sgd_train_partitioned(eegfx_ctx* ctx, const double* X, const double* y,
+                                       int64_t n, int32_t d, int32_t num_iterations,
+                                       double step_size, double reg_param,
+                                       double mini_batch_fraction, double convergence_tol,
+                                       int32_t num_partitions, double* weights,
+                                       int32_t* iterations_run, int mem) {
+  return glm_sgd_train(kGradLogistic, ctx, X, y, n, d, num_iterations, step_size, reg_param,
+                       mini_batch_fraction, convergence_tol, num_partitions, weights,
+                       iterations_run, mem);
+}
+
 int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
                            int32_t num_iterations, double step_size, double reg_param,
                            double mini_batch_fraction, double convergence_tol, double* weights,
                            int32_t* iterations_run, int mem) {
+  // Spark local[*] (SparkInitializer.java:44): defaultParallelism = the host's cores
+  const int32_t parts = (int32_t)std::max(1u, std::thread::hardware_concurrency());
   return glm_sgd_train(kGradLogistic, ctx, X, y, n, d, num_iterations, step_size, reg_param,
-                       mini_batch_fraction, convergence_tol, weights, iterations_run, mem);
+                       mini_batch_fraction, convergence_tol, parts, weights, iterations_run, mem);
+}
+
+int eegfx_spark_sample(int64_t n, double fraction, int32_t num_partitions, int64_t seed,
+                       uint32_t* mask, int64_t* kept) {
+  return guarded([&] {
+    if (n < 0 || num_partitions < 1 || !mask || !kept) fail(EEGFX_EINVAL, "bad argument");
+    if (!(fraction >= -1e-6 && fraction <= 1.0 + 1e-6))
+      fail(EEGFX_EINVAL, "Sampling fraction (%g) must be on interval [0, 1]", fraction);
+    *kept = spark::sample_mask(n, fraction, num_partitions, seed, mask);
+  });
 }
 
 int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
@@ -1186,7 +1248,7 @@ int eegfx_svm_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_
                         double mini_batch_fraction, double convergence_tol, double* weights,
                         int32_t* iterations_run, int mem) {
   return glm_sgd_train(kGradHinge, ctx, X, y, n, d, num_iterations, step_size, reg_param,
-                       mini_batch_fraction, convergence_tol, weights, iterations_run, mem);
+                       mini_batch_fraction, convergence_tol, 1, weights, iterations_run, mem);
 }
 
 int eegfx_svm_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d, const double* weights,

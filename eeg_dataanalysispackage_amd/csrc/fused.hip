@@ -316,42 +316,54 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
   }
 }
 
-// One sub-tile (8 epochs x C channels) per workgroup of C waves.  The windows land by LDS-DMA
-// (NT: non-temporal, when neighbouring windows do not overlap); after the barrier that publishes
-// them each lane decodes its 64 + 8 samples straight from LDS inside level 1, the cascade runs
-// in registers with cross-lane halos (ds_bpermute), the a6/d6 rows overwrite the start of the
-// window buffer once every wave has read its samples (26 KB of LDS per workgroup: 6 workgroups,
-// 18 waves per CU), and one wave normalises and stores the 8 rows.
-template <int CT, int C, bool FAST, bool NT>
-__global__ __launch_bounds__(64 * C, 5) void window_kernel(
+// SUBS sub-tiles (8 epochs x C channels each) per workgroup of C * SUBS waves: wave w works on
+// channel w % C of sub-tile w / C.  The windows land by LDS-DMA (NT: non-temporal, when
+// neighbouring windows do not overlap); after the barrier that publishes them each lane decodes
+// its 64 + 8 samples straight from LDS inside level 1, the cascade runs in registers with
+// cross-lane halos (ds_bpermute), the a6/d6 rows overwrite the start of their sub-tile's window
+// buffer once every wave has read its samples (26 KB of LDS per sub-tile: 6 sub-tiles, 18 waves
+// per CU), and one wave per sub-tile normalises and stores its 8 rows.  Each sub-tile's LDS is
+// laid out as a one-sub-tile workgroup's; the sub-tiles of a workgroup share only its barriers
+// and its dispatch.
+#ifndef EEGFX_WIN_SUBS
+#define EEGFX_WIN_SUBS 1
+#endif
+template <int CT, int C, bool FAST, bool NT, int SUBS = EEGFX_WIN_SUBS>
+__global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
     const float* __restrict__ base, int64_t n, double* __restrict__ out, Guard guard) {
   using G = Geometry<CT>;
   constexpr int F = C * 16;
   static_assert(kSub * F * 8 <= kSub * G::ESTR * 4, "feature rows alias the window buffer");
-  __shared__ __attribute__((aligned(16))) uint32_t win[kSub * G::ESTR];
-  __shared__ double norm[kSub];
-  __shared__ double gx[FAST ? kSub * C : 1];  // the guard's X^2 per signal (fma numerics)
+  __shared__ __attribute__((aligned(16))) uint32_t win_all[SUBS * kSub * G::ESTR];
+  __shared__ double norm_all[SUBS * kSub];
+  __shared__ double gx_all[FAST ? SUBS * kSub * C : 1];  // the guard's X^2 per signal (fma)
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = SUBS > 1 ? wid / C : 0, w = SUBS > 1 ? wid - h * C : wid;  // sub-tile, channel
+  uint32_t* win = win_all + h * kSub * G::ESTR;
+  double* norm = norm_all + h * kSub;
+  double* gx = gx_all + (FAST ? h * kSub * C : 0);
   const int el = lane >> 3, s = lane & 7;
   const int64_t nbytes = n_frames * G::FB;
   const int col = sel.col[w];
   const float r = sel.res[w];
-  const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * kSub;
-  const int64_t rest = n - e0;  // >= 1
-  const int ne = (rest >> 31) != 0 ? kSub : ((int)rest < kSub ? (int)rest : kSub);
+  const int64_t e0 = ((int64_t)xcd_tile(blockIdx.x, gridDim.x) * SUBS + h) * kSub;
+  const int64_t rest = n - e0;  // >= 1 for the first sub-tile; a later one may be empty
+  const int ne = rest <= 0 ? 0 : (rest >> 31) != 0 ? kSub : ((int)rest < kSub ? (int)rest : kSub);
 
   const bool mine = el < ne;
   // This lane's baseline and window word: loaded unconditionally (clamped to a valid epoch) and
   // used only once the window DMAs are in flight, so the prologue waits on one round trip (the
   // window words' scalar loads) before the DMAs leave instead of three.
-  const int elc = mine ? el : ne - 1;
-  const float b_ld = base[(e0 + elc) * C + w];
-  const uint32_t w_ld = (uint32_t)wb[e0 + elc];
+  const int64_t ec = SUBS > 1 && ne == 0 ? n - 1 : e0 + (mine ? el : ne - 1);
+  const float b_ld = base[ec * C + w];
+  const uint32_t w_ld = (uint32_t)wb[ec];
   const DmaRows<CT> rows(lane);
-  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
-    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  if (SUBS == 1 || ne > 0) {  // wave-uniform
+    if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+      dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  }
   const float b = mine ? b_ld : 0.0f;
   const int delta = mine ? (int)(w_ld & 14u) : 0;
   if (FAST && EEGFX_GUARD && (lane & 7) == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
@@ -359,11 +371,13 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   __syncthreads();
 
   // this lane's 64 samples + 8 halo samples of signal (epoch el, channel w), decoded in level 1
-  const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col;
-  const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
-  const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
-  double a6, d6;
-  cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);
+  double a6 = 0.0, d6 = 0.0;
+  if (SUBS == 1 || ne > 0) {
+    const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col;
+    const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
+    const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
+    cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);
+  }
 
   double* fb = (double*)win;
   __syncthreads();  // every wave has read its samples: the rows may overwrite the window
@@ -375,9 +389,10 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
   fb[slot] = a6;
   fb[slot + 8] = d6;
   __syncthreads();
-  if (w == 0) {
+  if (w == 0 && (SUBS == 1 || ne > 0)) {
     // the guard's rare path: the row recomputed under EXACT from the recording by this wave, with
-    // the LDS past the 8 feature rows as scratch (every other wave is done with the window)
+    // the LDS past the 8 feature rows of its sub-tile as scratch (every other wave is done with
+    // this sub-tile's window)
     auto redo = [&](int e, double* row) {
       const int64_t B = wb[e0 + e] & ~(int64_t)1;  // byte offset of the window (frame pos + 175)
       const int64_t f0 = B / G::FB;
@@ -393,33 +408,11 @@ __global__ __launch_bounds__(64 * C, 5) void window_kernel(
           },
           C, 16, fb + kSub * F, row, lane);
     };
-    // the guard's second stage: the row's measured max |x| per channel, from the staged window
-    // (epochs 1-7; epoch 0's window lies under the rows, so it is read from the recording)
+    // the guard's second stage: the row's measured max |x| per channel (recheck_c3), from the
+    // staged window (epochs 1-7; epoch 0's window lies under the rows: from the recording)
     auto recheck = [&](int e) {
-      const int64_t W = wb[e0 + e];
-      auto decode = [&](int c, float v) {
-        float y = v * sel.res[c];
-        y = y - base[(e0 + e) * C + c];
-        return (double)y;
-      };
-      if (e == 0) {  // uniform
-        const int64_t B = W & ~(int64_t)1;
-        const int64_t f0 = B / G::FB;
-        return guard_measured_x2_wave(
-            [&](int c, int k) -> float {
-              return f0 + k < n_frames
-                         ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
-                         : 0.0f;
-            },
-            decode, C, lane);
-      }
-      const uint8_t* ebe = (const uint8_t*)(win + e * G::ESTR) + ((uint32_t)W & 14u);
-      return guard_measured_x2_wave(
-          [&](int c, int k) -> float {
-            return (float)*(const int16_t*)(ebe + 16 * G::SEGQ * (k >> 6) + G::FB * (k & 63) +
-                                            2 * sel.col[c]);
-          },
-          decode, C, lane);
+      return recheck_c3<G::FB, G::SEGQ>(raw, n_frames, sel, wb[e0 + e], base + (e0 + e) * C,
+                            (const uint8_t*)(win + e * G::ESTR), e == 0, lane);
     };
     normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo, recheck);
   }
@@ -480,11 +473,12 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
   const float* bs = (const float*)scratch;
   const int64_t* words = (const int64_t*)((const uint8_t*)scratch + window_words_offset(n, C));
   (void)pos;  // read by launch_fused_baseline, which wrote the window words
-  const dim3 g((unsigned)((n + dev::kSub - 1) / dev::kSub));
+  constexpr int subs = EEGFX_WIN_SUBS;
+  const dim3 g((unsigned)((n + dev::kSub * subs - 1) / (dev::kSub * subs)));
   const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
-#define EEGFX_WIN(FA, NTV)                                                                         \
-  hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192), 0, st, (const uint8_t*)raw, \
-                     n_frames, sel, words, bs, n, out, guard)
+#define EEGFX_WIN(FA, NTV)                                                                   \
+  hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192 * subs), 0, st,         \
+                     (const uint8_t*)raw, n_frames, sel, words, bs, n, out, guard)
   if (fast) { if (nt) EEGFX_WIN(true, true); else EEGFX_WIN(true, false); }
   else { if (nt) EEGFX_WIN(false, true); else EEGFX_WIN(false, false); }
 #undef EEGFX_WIN

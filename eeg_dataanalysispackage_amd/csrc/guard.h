@@ -72,40 +72,65 @@ __device__ __forceinline__ void guard_count_rechecked(const Guard& g, int rows) 
   if (g.rechecked && rows) atomicAdd(g.rechecked, (unsigned long long)rows);
 }
 
+// Wave-wide minimum of packed int16 pairs (every lane gets it): the 16 lanes of a DPP row by
+// quad_perm xor 1 / xor 2, row_half_mirror and row_mirror (no LDS), then across the four rows.
+__device__ __forceinline__ uint32_t wave_pk_min_i16(uint32_t v) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  auto mn = [](uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s2, a),
+                                                                  __builtin_bit_cast(s2, b)));
+  };
+  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  v = mn(v, (uint32_t)__shfl_xor((int)v, 16, 64));
+  return mn(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+}
+
+// Packs a lane's (min, max) of int16 samples as (min, ~max) so that one packed minimum reduces
+// both (min(~a, ~b) = ~max(a, b), no overflow); unpack with guard_unpack_min / _max.
+__device__ __forceinline__ uint32_t guard_pack_minmax(int mn, int mx) {
+  return ((uint32_t)mn & 0xFFFFu) | ((uint32_t)~mx << 16);
+}
+__device__ __forceinline__ int guard_unpack_min(uint32_t p) { return (int)(int16_t)(p & 0xFFFFu); }
+__device__ __forceinline__ int guard_unpack_max(uint32_t p) { return ~(int)(int16_t)(p >> 16); }
+
 // The second stage, by one wave (every lane calls it; the result is wave-uniform): sum over the
 // row's C signals of X_c^2, X_c = max_k |x_c[k]| over the 512 window samples, measured.
-// sample(c, k) returns the raw value of sample k of channel c as a float (int16 values are exact;
-// 0 for the zero padding past the recording's end); the decode x = fl(fl(raw * r) - b) is monotone
-// in raw, so X_c = max(|x(min raw)|, |x(max raw)|) with decode(c, v) the kernels' own fp32 decode.
-// 16 lanes per channel, four channels per pass.  The 2^-20 margin covers the rounding of the sum.
+// sample(c, k) returns the int16 raw value of sample k of channel c (0 for the zero padding past
+// the recording's end); the decode x = fl(fl(raw * r) - b) is monotone in raw, so X_c =
+// max(|x(min raw)|, |x(max raw)|) with decode(c, v) the kernels' own fp32 decode.  16 lanes (one
+// DPP row) per channel, four channels per pass; each lane's 32 reads are independent.  The
+// 2^-20 margin covers the rounding of the sum.
 template <typename Sample, typename Decode>
 __device__ __forceinline__ double guard_measured_x2_wave(Sample sample, Decode decode, int C,
                                                          int lane) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  auto mn = [](uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s2, a),
+                                                                  __builtin_bit_cast(s2, b)));
+  };
   const int grp = lane >> 4, l = lane & 15;
   double sx = 0.0;
 #pragma unroll 1
   for (int c0 = 0; c0 < C; c0 += 4) {
-    const int c = c0 + grp;
-    float lo = 0.0f, hi = 0.0f;
-    if (c < C) {
-      lo = hi = sample(c, l);
-#pragma unroll 4
-      for (int k = l + 16; k < 512; k += 16) {
-        const float v = sample(c, k);
-        lo = fminf(lo, v);
-        hi = fmaxf(hi, v);
-      }
+    const int c = c0 + grp < C ? c0 + grp : C - 1;
+    int lo = 32767, hi = -32768;
+#pragma unroll 8
+    for (int k = l; k < 512; k += 16) {
+      const int v = sample(c, k);
+      lo = min(lo, v);
+      hi = max(hi, v);
     }
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-      lo = fminf(lo, __shfl_xor(lo, off, 64));
-      hi = fmaxf(hi, __shfl_xor(hi, off, 64));
-    }
-    double x2 = 0.0;
-    if (c < C) {
-      const double X = fmax(fabs(decode(c, lo)), fabs(decode(c, hi)));
-      x2 = X * X;
-    }
+    uint32_t p = guard_pack_minmax(lo, hi);  // reduced over the DPP row = this channel's lanes
+    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0xB1, 0xF, 0xF, false));
+    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x4E, 0xF, 0xF, false));
+    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x141, 0xF, 0xF, false));
+    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x140, 0xF, 0xF, false));
+    const double X = fmax(fabs(decode(c, (float)guard_unpack_min(p))),
+                          fabs(decode(c, (float)guard_unpack_max(p))));
+    double x2 = c0 + grp < C ? X * X : 0.0;
     x2 += __shfl_xor(x2, 16, 64);
     x2 += __shfl_xor(x2, 32, 64);
     sx += x2;

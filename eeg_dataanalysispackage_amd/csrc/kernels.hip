@@ -212,7 +212,7 @@ __device__ __forceinline__ void staged_features(Smp smp, GSmp gsmp, const int* s
         if (lane == 0) guard_count_rechecked(guard, 1);
         fails = guard_fails(acc, kGuardK2Collapsed,
                             guard_measured_x2_wave(
-                                [&](int c, int k) { return gsmp(175 + k, s_col[c]); },
+                                [&](int c, int k) { return (int)gsmp(175 + k, s_col[c]); },
                                 [&](int c, float v) {
                                   float y = v * s_res[c];
                                   y = y - s_base[c];
@@ -408,17 +408,8 @@ __global__ __launch_bounds__(256) void cut_features_c3_kernel(
     };
     // the guard's second stage: the row's measured max |x| per channel, from the recording
     auto recheck = [&](int e) {
-      const int64_t f0 = sP[e] + 175;
-      return guard_measured_x2_wave(
-          [&](int cc, int k) -> float {
-            return f0 + k < n_frames ? (float)raw[(f0 + k) * CT + s_col[cc]] : 0.0f;
-          },
-          [&](int cc, float v) {
-            float y = v * s_res[cc];
-            y = y - s_base[e * C + cc];
-            return (double)y;
-          },
-          C, lane);
+      return recheck_c3<FB, 1>((const uint8_t*)raw, n_frames, sel, (sP[e] + 175) * FB,
+                            s_base + e * C, nullptr, true, lane);
     };
     normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo, recheck);
   }

@@ -93,9 +93,10 @@ hipError_t launch_guard_fixup_raw(hipStream_t st, const void* raw, int fmt, int6
 // logreg.hip: MLlib LogisticRegressionWithSGD (full batch) on device.  State block: iteration
 // count, flag (0 running, 1 converged / done, 2 invalid labels), then the d weights.
 struct LrState {
-  int32_t iter;
-  int32_t converged;
-  int32_t pad[2];
+  int32_t iter;       // iterations done (GradientDescent's i - 1)
+  int32_t converged;  // 1: converged or done, 2: label validation failed
+  int32_t updates;    // iterations that updated the weights (a non-empty mini-batch)
+  int32_t pad;
   double w[];
 };
 constexpr int kLrMaxFeatures = 1024;
@@ -116,9 +117,12 @@ hipError_t launch_lr_validate(hipStream_t st, const double* y, int64_t n, LrStat
 // kernel scores with the matching model (sigmoid of the margin / the margin itself).
 constexpr int kGradLogistic = 0;
 constexpr int kGradHinge = 1;
+// mask: iteration's mini-batch sample (bit r of word r / 32 = row r), nullptr = the whole batch;
+// count = its rows (the gradient's divisor; 0 = an empty sample: no update)
 hipError_t launch_lr_iteration(hipStream_t st, int grad, const double* X, const double* y,
-                               int64_t n, int d, LrState* state, double* partial, int G,
-                               double step_size, double reg, double tol, int max_iter);
+                               int64_t n, int d, const uint32_t* mask, int64_t count,
+                               LrState* state, double* partial, int G, double step_size,
+                               double reg, double tol, int max_iter);
 hipError_t launch_lr_predict(hipStream_t st, int grad, const double* X, int64_t n, int d,
                              const double* w, double intercept, double threshold,
                              int use_threshold, double* out);

@@ -1,8 +1,10 @@
 // logreg.hip -- the classifier the reference trains on the feature matrix, on the GPU
 // (SURVEY.md 8f rank 4): Spark MLlib 1.6.2 LogisticRegressionWithSGD as called by
-// Classification/LogisticRegressionClassifier.java:85-114, i.e. full-batch gradient descent
-// (miniBatchFraction 1.0) with LogisticGradient, SquaredL2Updater and GradientDescent's
-// convergence test, no intercept; and LogisticRegressionModel.predict for :117-141.
+// Classification/LogisticRegressionClassifier.java:85-114, i.e. gradient descent with
+// LogisticGradient, SquaredL2Updater and GradientDescent's convergence test, no intercept, over
+// the whole batch or (miniBatchFraction < 1) over the rows of iteration i's sample, a bit mask
+// the host draws with Spark's own sampler (api.cpp spark_sample_mask); and
+// LogisticRegressionModel.predict for :117-141.
 //
 // One iteration = two launches on the context stream, no host round trip:
 //   lr_grad_kernel    G workgroups x 4 waves.  Row r goes to wave r mod (4G); a wave's 64 lanes
@@ -53,10 +55,16 @@ __device__ __forceinline__ double grad_mult(double margin, double y) {
   }
 }
 
+// Row r of iteration's sample (mask == nullptr: every row).
+__device__ __forceinline__ bool sampled(const uint32_t* __restrict__ mask, int64_t r) {
+  return !mask || ((mask[r >> 5] >> (r & 31)) & 1u);
+}
+
 template <int KD, int GRAD>  // features per lane: d <= 64 * KD
 __global__ __launch_bounds__(64 * kLrWaves) void lr_grad_kernel(
     const double* __restrict__ X, const double* __restrict__ y, int64_t n, int d,
-    const LrState* __restrict__ st, double* __restrict__ partial) {
+    const uint32_t* __restrict__ mask, const LrState* __restrict__ st,
+    double* __restrict__ partial) {
   if (st->converged) return;
   __shared__ double acc_s[kLrWaves][64 * KD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -70,6 +78,7 @@ __global__ __launch_bounds__(64 * kLrWaves) void lr_grad_kernel(
   }
   const int64_t stride = (int64_t)gridDim.x * kLrWaves;
   for (int64_t r = (int64_t)blockIdx.x * kLrWaves + w; r < n; r += stride) {
+    if (!sampled(mask, r)) continue;  // wave-uniform: one row per wave
     const double* row = X + r * d;
     double x[KD];
     double dot = 0.0;
@@ -118,7 +127,8 @@ __device__ __forceinline__ double row16_sum(double v) {
 template <int FPL, int GRAD>
 __global__ __launch_bounds__(64 * kLrWaves) void lr_grad16_kernel(
     const double* __restrict__ X, const double* __restrict__ y, int64_t n, int d,
-    const LrState* __restrict__ st, double* __restrict__ partial) {
+    const uint32_t* __restrict__ mask, const LrState* __restrict__ st,
+    double* __restrict__ partial) {
   if (st->converged) return;
   __shared__ double acc_s[kLrWaves * 4][16 * FPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(64 * kLrWaves) void lr_grad16_kernel(
       const int64_t r = r0 + 4 * u + q;
       dot[u] = 0.0;
       if constexpr (GRAD == 0) {
-        const bool ok = r < n;
+        const bool ok = r < n && sampled(mask, r);
         const double* row = X + (ok ? r : 0) * d;
 #pragma unroll
         for (int k = 0; k < FPL; ++k) {
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(64 * kLrWaves) void lr_grad16_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const double m = row16_sum(dot[u]);
-      const bool ok = r0 + 4 * u + q < n;
+      const bool ok = r0 + 4 * u + q < n && sampled(mask, r0 + 4 * u + q);
       const double mult = ok ? grad_mult<GRAD>(m, yy[u]) : 0.0;
 #pragma unroll
       for (int k = 0; k < FPL; ++k) acc[k] = __builtin_fma(mult, x[u][k], acc[k]);
@@ -240,10 +250,21 @@ __global__ __launch_bounds__(256) void lr_update_kernel(const double* __restrict
   }
   if (threadIdx.x == 0) {
     st->iter = it;
-    // GradientDescent.isConverged, checked once two iterates exist (i >= 2)
+    const int up = st->updates + 1;
+    st->updates = up;
+    // GradientDescent.isConverged, checked once two updated iterates exist (with a full batch:
+    // from iteration 2; an empty mini-batch updates nothing and tests nothing)
     const double diff = sqrt(red[0][0]), nrm = sqrt(red[1][0]);
-    if ((it >= 2 && diff < tol * (nrm > 1.0 ? nrm : 1.0)) || it >= max_iter) st->converged = 1;
+    if ((up >= 2 && diff < tol * (nrm > 1.0 ? nrm : 1.0)) || it >= max_iter) st->converged = 1;
   }
+}
+
+// An iteration whose mini-batch sample is empty (GradientDescent: "The size of sampled batch is
+// zero"): i advances, the weights and the convergence state do not.
+__global__ void lr_skip_kernel(int max_iter, LrState* __restrict__ st) {
+  if (st->converged || threadIdx.x != 0) return;
+  st->iter += 1;
+  if (st->iter >= max_iter) st->converged = 1;
 }
 
 // KIND 0: LogisticRegressionModel.predictPoint (score = sigmoid(w.x + b)); KIND 1:
@@ -301,48 +322,55 @@ int lr_grid(int64_t n) {
 
 template <int GRAD>
 static hipError_t lr_iteration(hipStream_t st, const double* X, const double* y, int64_t n, int d,
-                               LrState* state, double* partial, int G, double step_size,
-                               double reg, double tol, int max_iter) {
+                               const uint32_t* mask, int64_t count, LrState* state,
+                               double* partial, int G, double step_size, double reg, double tol,
+                               int max_iter) {
+  if (count == 0) {
+    hipLaunchKernelGGL(dev::lr_skip_kernel, dim3(1), dim3(64), 0, st, max_iter, state);
+    return hipGetLastError();
+  }
   if (d <= 128) {
     const int fpl = (d + 15) / 16;
     switch (fpl <= 1 ? 1 : fpl <= 2 ? 2 : fpl <= 3 ? 3 : fpl <= 4 ? 4 : 8) {
       EEGFX_LR_KD(1, hipLaunchKernelGGL((dev::lr_grad16_kernel<1, GRAD>), dim3(G), dim3(256), 0,
-                                        st, X, y, n, d, state, partial))
+                                        st, X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(2, hipLaunchKernelGGL((dev::lr_grad16_kernel<2, GRAD>), dim3(G), dim3(256), 0,
-                                        st, X, y, n, d, state, partial))
+                                        st, X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(3, hipLaunchKernelGGL((dev::lr_grad16_kernel<3, GRAD>), dim3(G), dim3(256), 0,
-                                        st, X, y, n, d, state, partial))
+                                        st, X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(4, hipLaunchKernelGGL((dev::lr_grad16_kernel<4, GRAD>), dim3(G), dim3(256), 0,
-                                        st, X, y, n, d, state, partial))
+                                        st, X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(8, hipLaunchKernelGGL((dev::lr_grad16_kernel<8, GRAD>), dim3(G), dim3(256), 0,
-                                        st, X, y, n, d, state, partial))
+                                        st, X, y, n, d, mask, state, partial))
     }
   } else {
     const int kd = (d + 63) / 64;
     switch (kd <= 1 ? 1 : kd <= 2 ? 2 : kd <= 4 ? 4 : kd <= 8 ? 8 : 16) {
       EEGFX_LR_KD(1, hipLaunchKernelGGL((dev::lr_grad_kernel<1, GRAD>), dim3(G), dim3(256), 0, st,
-                                        X, y, n, d, state, partial))
+                                        X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(2, hipLaunchKernelGGL((dev::lr_grad_kernel<2, GRAD>), dim3(G), dim3(256), 0, st,
-                                        X, y, n, d, state, partial))
+                                        X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(4, hipLaunchKernelGGL((dev::lr_grad_kernel<4, GRAD>), dim3(G), dim3(256), 0, st,
-                                        X, y, n, d, state, partial))
+                                        X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(8, hipLaunchKernelGGL((dev::lr_grad_kernel<8, GRAD>), dim3(G), dim3(256), 0, st,
-                                        X, y, n, d, state, partial))
+                                        X, y, n, d, mask, state, partial))
       EEGFX_LR_KD(16, hipLaunchKernelGGL((dev::lr_grad_kernel<16, GRAD>), dim3(G), dim3(256), 0,
-                                         st, X, y, n, d, state, partial))
+                                         st, X, y, n, d, mask, state, partial))
     }
   }
-  hipLaunchKernelGGL(dev::lr_update_kernel, dim3(1), dim3(256), 0, st, partial, G, n, d,
+  hipLaunchKernelGGL(dev::lr_update_kernel, dim3(1), dim3(256), 0, st, partial, G, count, d,
                      step_size, reg, tol, max_iter, state);
   return hipGetLastError();
 }
 
 hipError_t launch_lr_iteration(hipStream_t st, int grad, const double* X, const double* y,
-                               int64_t n, int d, LrState* state, double* partial, int G,
-                               double step_size, double reg, double tol, int max_iter) {
-  return grad == kGradHinge
-             ? lr_iteration<1>(st, X, y, n, d, state, partial, G, step_size, reg, tol, max_iter)
-             : lr_iteration<0>(st, X, y, n, d, state, partial, G, step_size, reg, tol, max_iter);
+                               int64_t n, int d, const uint32_t* mask, int64_t count,
+                               LrState* state, double* partial, int G, double step_size,
+                               double reg, double tol, int max_iter) {
+  return grad == kGradHinge ? lr_iteration<1>(st, X, y, n, d, mask, count, state, partial, G,
+                                              step_size, reg, tol, max_iter)
+                            : lr_iteration<0>(st, X, y, n, d, mask, count, state, partial, G,
+                                              step_size, reg, tol, max_iter);
 }
 
 template <int KIND>

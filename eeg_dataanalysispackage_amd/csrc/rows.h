@@ -8,6 +8,7 @@
 
 #include "dwt8.h"
 #include "guard.h"
+#include "launch.h"
 
 namespace eegfx {
 namespace dev {
@@ -107,6 +108,59 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
     *(double2*)(o + i) = make_double2(v0, v1);
   }
   wave_sync();
+}
+
+// The conditioning guard's second stage (guard.h) for one row of the 3-channel kernels, by one
+// wave: lane l reads frames 64 (l >> 3) + 8 (l & 7) .. + 7 of the window, all three channels --
+// from the staged window `lds` (the window kernel's layout: segment s at 16 SEGQ s bytes past the
+// epoch's misalignment) or, when from_raw, from the recording (zero past its end, the reference's
+// padding) -- keeps each channel's min and max raw sample, reduces them over the wave as packed
+// int16 pairs (DPP, no LDS round trips), and returns sum_c X_c^2 with X_c = max(|x(min)|,
+// |x(max)|): x = fl(fl(raw * r) - b) is monotone in raw.  One LDS (or memory) round trip for all
+// 24 samples of a lane.
+template <int FB, int SEGQ>
+__device__ __forceinline__ double recheck_c3(const uint8_t* __restrict__ raw, int64_t n_frames,
+                                             const ChanSel& sel, int64_t W,
+                                             const float* __restrict__ b, const uint8_t* lds,
+                                             bool from_raw, int lane) {
+  const int f0 = 8 * lane;  // = 64 (lane >> 3) + 8 (lane & 7)
+  int v[3][8];
+  if (from_raw) {  // wave-uniform
+    const int64_t B = W & ~(int64_t)1;
+    const int64_t g0 = B / FB + f0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        v[c][i] = g0 + i < n_frames
+                      ? *(const int16_t*)(raw + B + (int64_t)(f0 + i) * FB + 2 * sel.col[c])
+                      : 0;
+  } else {
+    const uint8_t* p = lds + ((uint32_t)W & 14u) + 16 * SEGQ * (lane >> 3) +
+                       FB * 8 * (lane & 7);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c][i] = *(const int16_t*)(p + FB * i + 2 * sel.col[c]);
+  }
+  double sx = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int mn = v[c][0], mx = v[c][0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+      mn = min(mn, v[c][i]);
+      mx = max(mx, v[c][i]);
+    }
+    const uint32_t pr = wave_pk_min_i16(guard_pack_minmax(mn, mx));
+    const float r = sel.res[c], bc = b[c];
+    float lo = (float)guard_unpack_min(pr) * r, hi = (float)guard_unpack_max(pr) * r;
+    lo = lo - bc;
+    hi = hi - bc;
+    const double X = fmax(fabs((double)lo), fabs((double)hi));
+    sx += X * X;
+  }
+  return sx * (1.0 + 0x1p-20);
 }
 
 }  // namespace dev

@@ -259,9 +259,9 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
         fails = guard_fails(
             acc, kGuardK2Collapsed,
             guard_measured_x2_wave(
-                [&](int c, int k) -> float {
-                  return sample_at<T>(eb + sel.col[c] * (int)sizeof(T) + 16 * SEGQ * (k >> 6) +
-                                      FB * (k & 63));
+                [&](int c, int k) -> int {
+                  return (int)sample_at<T>(eb + sel.col[c] * (int)sizeof(T) + 16 * SEGQ * (k >> 6) +
+                                           FB * (k & 63));
                 },
                 [&](int c, float v) {
                   float y = v * sel.res[c];
@@ -402,9 +402,9 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
         fails = guard_fails(
             acc, kGuardK2Collapsed,
             guard_measured_x2_wave(
-                [&](int cc, int k) -> float {
-                  return (float)sample_at<int16_t>(win + (int)(B & 15) + sel.col[cc] * 2 +
-                                                   16 * SEGQ * (k >> 6) + FB * (k & 63));
+                [&](int cc, int k) -> int {
+                  return *(const int16_t*)(win + (int)(B & 15) + sel.col[cc] * 2 +
+                                           16 * SEGQ * (k >> 6) + FB * (k & 63));
                 },
                 [&](int cc, float v) {
                   float y = v * sel.res[cc];

@@ -256,9 +256,9 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
  * step/sqrt(i), GradientDescent's convergence test (||w_prev - w|| < tol * max(||w||, 1), MLlib's
  * tol = 0.001), no intercept.  X is n x d row-major (the feature matrix as produced), y the 0/1
  * labels; `weights` holds the initial weights (zeros in MLlib) on entry and the trained ones on
- * return (host array).  mini_batch_fraction must be 1.0 (EEGFX_ENOTSUP otherwise: Spark's sampler
- * depends on its partitioning); labels other than 0/1 give EEGFX_EINVAL ("Input validation
- * failed").  eegfx_logreg_predict: LogisticRegressionModel.predict -- score = 1/(1+exp(-(w.x+b))),
+ * return (host array).  mini_batch_fraction < 1 samples each iteration's mini-batch as MLlib does
+ * (eegfx_logreg_sgd_train_partitioned below); labels other than 0/1 give EEGFX_EINVAL ("Input
+ * validation failed").  eegfx_logreg_predict: LogisticRegressionModel.predict -- score = 1/(1+exp(-(w.x+b))),
  * out = score > threshold ? 1 : 0, or the score itself when threshold is NaN (clearThreshold). */
 int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,
                            int32_t num_iterations, double step_size, double reg_param,
@@ -267,6 +267,25 @@ int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int
 int eegfx_logreg_predict(eegfx_ctx* ctx, const double* X, int64_t n, int32_t d,
                          const double* weights, double intercept, double threshold, double* out,
                          int mem);
+/* The same training with the Spark partition count stated.  mini_batch_fraction f in [0, 1)
+ * (config_mini_batch_fraction, LogisticRegressionClassifier.java:98-108, README.md:136): iteration
+ * i (1-based) trains on MLlib's data.sample(false, f, 42 + i) of the n rows split into
+ * num_partitions ParallelCollectionRDD slices (partition p: rows [p n / N, (p + 1) n / N)), the
+ * sample drawn on the host with Spark 1.6.2's own sampler (PartitionwiseSampledRDD seeds from
+ * java.util.Random, BernoulliSampler / GapSamplingIterator on XORShiftRandom; eegfx_spark_sample)
+ * and the gradient divided by the sample size; an empty sample skips the update.  f >= 1: the
+ * full batch.  eegfx_logreg_sgd_train is this function with num_partitions = the host's hardware
+ * threads (Spark local[*]'s defaultParallelism, SparkInitializer.java:44). */
+int eegfx_logreg_sgd_train_partitioned(eegfx_ctx* ctx, const double* X, const double* y,
+                                       int64_t n, int32_t d, int32_t num_iterations,
+                                       double step_size, double reg_param,
+                                       double mini_batch_fraction, double convergence_tol,
+                                       int32_t num_partitions, double* weights,
+                                       int32_t* iterations_run, int mem);
+/* RDD.sample(false, fraction, seed) of n rows in num_partitions slices (pure host function):
+ * mask = bit r of word r / 32 set for every kept row ((n + 31) / 32 words), *kept = their count. */
+int eegfx_spark_sample(int64_t n, double fraction, int32_t num_partitions, int64_t seed,
+                       uint32_t* mask, int64_t* kept);
 
 /* eegfx_svm_* (MLlib SVMWithSGD on the same device loop) is declared in eegfx_ext.h: SURVEY.md
  * section 2 marks the SVM classifier out of the hot-path scope, so it is not part of this contract. */

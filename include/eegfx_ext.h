@@ -18,7 +18,8 @@ extern "C" {
  * (s = 2y - 1; rows with 1 > s * w.x add -s * x to the gradient) -- the default constructor (step
  * 1.0, 100 iterations, regParam 0.01, fraction 1.0) or, with the config_* keys, the static
  * train(rdd, iterations, step, config_reg_param, fraction).  Same arguments, errors and device
- * loop as eegfx_logreg_sgd_train.  eegfx_svm_predict: SVMModel.predict (SVMClassifier.java:71) --
+ * loop as eegfx_logreg_sgd_train, full batch only (mini_batch_fraction < 1: EEGFX_ENOTSUP).
+ * eegfx_svm_predict: SVMModel.predict (SVMClassifier.java:71) --
  * margin = w.x + b, out = margin > threshold ? 1 : 0 (MLlib's default threshold 0.0), or the
  * margin itself when threshold is NaN (clearThreshold). */
 int eegfx_svm_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int64_t n, int32_t d,

@@ -109,11 +109,58 @@ def test_errors(ctx):
         clf.sgd_train(ctx, X, y)
     y[7] = 1.0
     with pytest.raises(fx.EegfxError):
-        clf.sgd_train(ctx, X, y, mini_batch_fraction=0.5)  # Spark's partitioned sampler
+        clf.sgd_train(ctx, X, y, mini_batch_fraction=1.5)  # BernoulliSampler's require
+    with pytest.raises(fx.EegfxError):
+        clf.sgd_train(ctx, X, y, mini_batch_fraction=0.5, num_partitions=0)
+    with pytest.raises(fx.EegfxError):
+        clf.svm_sgd_train(ctx, X, y, mini_batch_fraction=0.5)  # the SVM loop stays full-batch
     with pytest.raises(fx.EegfxError):
         clf.sgd_train(ctx, np.zeros((0, 48)), np.zeros(0))
     with pytest.raises(fx.EegfxError):
         clf.sgd_train(ctx, np.zeros((4, 2000)), np.zeros(4))
+
+
+@pytest.mark.parametrize("f", [0.1, 0.5, 0.03])
+@pytest.mark.parametrize("n,parts", [(5000, 16), (2000, 3), (40, 8)])
+def test_mini_batch_sgd_matches_mllib_restatement(ctx, n, parts, f):
+    """config_mini_batch_fraction < 1 (LogisticRegressionClassifier.java:98-108, README.md:136):
+    iteration i trains on MLlib's data.sample(false, f, 42 + i) over `parts` Spark partitions;
+    weights within the full-batch tolerance of the restatement, same iteration count (parity
+    unpinned: no reference fixture holds weights or samples).  n = 40 at f = 0.03 has empty
+    samples: those iterations update nothing."""
+    X, y = rows(n, 48, n + parts)
+    for reg, tol in ((0.0, 0.001), (0.01, 0.3)):
+        w, it = clf.sgd_train(ctx, X, y, 100, 1.0, reg, mini_batch_fraction=f,
+                              convergence_tol=tol, num_partitions=parts)
+        wr, itr = ref.sgd_train(X, y, 100, 1.0, reg, convergence_tol=tol, mini_batch_fraction=f,
+                                num_partitions=parts)
+        assert it == itr, (reg, it, itr)
+        assert close(w, wr)
+    if n == 40 and f == 0.03:
+        empty = [i for i in range(1, 101) if not ref.sample_rows(n, f, parts, 42 + i)]
+        assert empty   # the case this parameter set exists for
+
+
+def test_mini_batch_device_inputs_and_classifier_config(ctx):
+    X, y = rows(3000, 48, 11)
+    w, it = clf.sgd_train(ctx, torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), 50, 0.5,
+                          0.0, mini_batch_fraction=0.25, num_partitions=4)
+    wr, itr = ref.sgd_train(X, y, 50, 0.5, 0.0, mini_batch_fraction=0.25, num_partitions=4)
+    assert it == itr and close(w, wr)
+    # the classifier's config path (static train(rdd, iterations, step, fraction), regParam 0)
+    odp = fx.OffLineDataProvider([INFO_TRAIN], context=ctx)
+    odp.loadData()
+    fe = fx.WaveletTransform(8, 512, 175, 16, context=ctx)
+    c = clf.LogisticRegressionClassifier(context=ctx)
+    c.num_partitions = 4
+    c.setConfig({"config_num_iterations": "20", "config_step_size": "1.0",
+                 "config_mini_batch_fraction": "0.5"})
+    data, labels = odp.getData(), odp.getDataLabels()
+    c.train(data, labels, fe)
+    feats = fe.extractFeaturesBatch(data)
+    wr, itr = ref.sgd_train(feats, np.asarray(labels), 20, 1.0, 0.0, mini_batch_fraction=0.5,
+                            num_partitions=4)
+    assert c.iterations_run == itr and close(c.weights, wr)
 
 
 def test_classifier_flow_on_info_txt(ctx):

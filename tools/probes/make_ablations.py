@@ -16,8 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "..", "eeg_dataanalysispackage_amd", "csrc")
 FILES = ("fused.hip", "wide.hip", "dwt8.h")
 
-DMA_ISSUE = """  if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
-    dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);"""
+DMA_ISSUE = """    if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+      dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);"""
 
 FMA_BODY = """#pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -73,7 +73,7 @@ ABLATIONS = {
         "no window DMA: removes the HBM window reads and the LDS writes; LDS reads, decode and "
         "fp64 kept (wrong results)",
         [("fused.hip", DMA_ISSUE,
-          "  (void)rows;  // ablation: no window DMA (no HBM window reads, no LDS writes)")]),
+          "    (void)rows;  // ablation: no window DMA (no HBM window reads, no LDS writes)")]),
     "l2src": (
         "window DMA from a 2 MB L2-resident region (same addresses mod 2 MB): removes HBM reads "
         "only (wrong results)",
@@ -83,22 +83,20 @@ ABLATIONS = {
         "no LDS staging: each lane loads its 64 samples (128 B, L2-resident region) into VGPRs; "
         "no window DMA, no LDS sample reads (wrong results)",
         [("fused.hip", DMA_ISSUE,
-          "  (void)rows;  // ablation: no LDS staging; the lane's 64 samples come from VGPRs"),
-         ("fused.hip", """  double a6, d6;
-  cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);""",
-          """  double a6, d6;
-  (void)own; (void)nxt;
-  u32x4_a4 q[8];
-  {
-    const int64_t wv = mine ? wb[e0 + el] : 0;
-    const u32x4_a16* src = (const u32x4_a16*)(raw + ((wv + 384 * s + 128 * w) & 0x1FFFF0));
+          "    (void)rows;  // ablation: no LDS staging; the lane's 64 samples come from VGPRs"),
+         ("fused.hip", """    cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);""",
+          """    (void)own; (void)nxt;
+    u32x4_a4 q[8];
+    {
+      const int64_t wv = mine ? wb[e0 + el] : 0;
+      const u32x4_a16* src = (const u32x4_a16*)(raw + ((wv + 384 * s + 128 * w) & 0x1FFFF0));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) q[i] = src[i];
-  }
-  dwt8_collapsed_cascade([&](int k) {
-    const uint32_t v = q[k >> 3][(k >> 1) & 3];
-    return (float)(int16_t)((k & 1) ? (v >> 16) : (v & 0xffffu));
-  }, r, b, lane & ~7, s, a6, d6);""")]),
+      for (int i = 0; i < 8; ++i) q[i] = src[i];
+    }
+    dwt8_collapsed_cascade([&](int k) {
+      const uint32_t v = q[k >> 3][(k >> 1) & 3];
+      return (float)(int16_t)((k & 1) ? (v >> 16) : (v & 0xffffu));
+    }, r, b, lane & ~7, s, a6, d6);""")]),
     "noldsread": (
         "no LDS sample reads: each sample is an opaque per-lane float plus its index (one fp32 "
         "add in place of the int16 conversion); window DMA, decode and fp64 kept (wrong results)",

@@ -1,0 +1,30 @@
+# (1) GPU tests of this round's changes: the guard's second stage (every int16 fma kernel), the
+#     mini-batch logistic regression, the Java shim's call sequence from C;
+# (2) the guard's flag-rate study on the fast second stage (--plant flat / null);
+# (3) window kernel with 1, 2, 3 sub-tiles per workgroup (EEGFX_WIN_SUBS, probes wp_s1..3):
+#     window and step, interleaved, three repetitions.
+set -uo pipefail
+OUT=gpurun_out/r05c
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_guard.py tests/test_gpu_logreg.py tests/test_gpu_c_abi.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+tail -3 $OUT/pytest.log
+B="--cpu-sample 0 --alt-steps 0 --steps 50 --warmup 20"
+for spec in none flat:0.01 flat:0.1 flat:0.32 flat:1.0 null:0.01 null:0.1 null:0.32; do
+  if [ $spec = none ]; then PL=""; else PL="--plant $spec"; fi
+  timeout -k 10 300 python bench.py $B $PL > $OUT/plant_${spec/:/_}.json 2> $OUT/plant_${spec/:/_}.err || { tail -20 $OUT/plant_${spec/:/_}.err; exit 1; }
+  python3 -c "
+import json
+d = json.load(open('$OUT/plant_${spec/:/_}.json'))
+g = d['config']['guard']
+print('$spec', 'step ms', d['ms_per_step'], 'window ms', d['roofline']['kernel_ms'], 'checked', g['rows_checked'], 'rechecked', g['rows_rechecked'], 'recomputed', g['rows_recomputed'])
+"
+done
+P=tools/probes/r05
+for rep in 1 2 3; do
+  for v in wp_s1 wp_s2 wp_s3; do
+    timeout -k 10 60 $P/$v >> $OUT/subs_window.log 2>&1 || { echo "$v failed"; tail -3 $OUT/subs_window.log; exit 1; }
+    PROBE_STEP=1 timeout -k 10 60 $P/$v >> $OUT/subs_step.log 2>&1 || { echo "$v step failed"; exit 1; }
+  done
+done
+echo "== window (s1 s2 s3 x3)"; cat $OUT/subs_window.log; echo "== step"; cat $OUT/subs_step.log
