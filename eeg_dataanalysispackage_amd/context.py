@@ -149,6 +149,12 @@ class Context:
                                           1 if reset else 0))
         return int(a.value), int(b.value)
 
+    def set_mailbox(self, enable: bool) -> None:
+        """Opt-in resident server for small host extract batches (eegfx_ctx_set_mailbox): the
+        per-epoch drop-in without a launch per call.  Disable it before a device-wide
+        synchronisation (torch.cuda.synchronize), which would wait for the resident kernel."""
+        check(lib().eegfx_ctx_set_mailbox(self.handle, 1 if enable else 0))
+
     def guard_detail(self, reset: bool = False):
         """(rows checked, rows that went to the guard's second stage, rows recomputed under EXACT)
         since the context was created or last reset (eegfx_ctx_guard_detail; synchronises)."""

@@ -206,7 +206,72 @@ struct eegfx_ctx {
     }
     HIP_CHECK(e);
   }
+  // The opt-in resident small-batch server (eegfx_ctx_set_mailbox, features_mailbox_kernel): a
+  // host-mapped command block, the kernel's own stream (never the context stream: the kernel
+  // stays resident), the request sequence and the time of the last request.
+  bool mailbox = false;
+  hipStream_t mb_stream = nullptr;
+  MailboxCmd* mb_host = nullptr;
+  MailboxCmd* mb_dev = nullptr;
+  uint32_t mb_seq = 0;
+  bool mb_live = false;  // launched and not stopped by the host (it may still have idled out)
+  std::chrono::steady_clock::time_point mb_last{};
+  static constexpr uint64_t kMbIdleTicks = 100000000;  // 1 s of s_memrealtime (100 MHz)
+  void mb_launch() {
+    const Guard g{guard_dev, nullptr, (unsigned long long*)(guard_dev + 2),
+                  (unsigned long long*)(guard_dev + 4)};
+    HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks, g));
+    mb_live = true;
+  }
+  void mb_stop() {
+    if (!mb_host) return;
+    __atomic_store_n(&mb_host->stop, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(mb_stream);  // the kernel sees `stop` within one poll
+    __atomic_store_n(&mb_host->stop, 0u, __ATOMIC_RELEASE);
+    mb_live = false;
+  }
+  // One request: n epochs of packed window rows in pin_in -> rows in pin_out.
+  void mb_serve(int64_t n, int C, int nfeat) {
+    MailboxCmd* m = mb_host;
+    m->n = n;
+    m->C = C;
+    m->nfeat = nfeat;
+    m->fast = numerics != EEGFX_EXACT ? 1 : 0;
+    m->rows = (const double*)pin_in.device_ptr();
+    m->out = (double*)pin_out.device_ptr();
+    if (++mb_seq == 0) mb_seq = 1;  // 0 means "no request" to the kernel
+    const auto now = std::chrono::steady_clock::now();
+    // the kernel returns after 1 s without a request: relaunch it when it may have
+    if (!mb_live ||
+        (now - mb_last > std::chrono::milliseconds(500) && hipStreamQuery(mb_stream) == hipSuccess))
+      mb_launch();
+    __atomic_store_n(&m->req, mb_seq, __ATOMIC_RELEASE);
+    for (uint64_t spin = 1;; ++spin) {
+      if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == mb_seq) break;
+      if ((spin & 4095) == 0) {
+        // the kernel went idle between the check above and the request: serve it again
+        if (hipStreamQuery(mb_stream) == hipSuccess &&
+            __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != mb_seq)
+          mb_launch();
+        if (std::chrono::steady_clock::now() - now > std::chrono::seconds(30))
+          fail(EEGFX_EHIP, "mailbox request %u not served within 30 s", mb_seq);
+      }
+      __builtin_ia32_pause();
+    }
+    mb_last = std::chrono::steady_clock::now();
+  }
+  void release_mailbox() {
+    if (!mb_host) return;
+    mb_stop();
+    (void)hipStreamDestroy(mb_stream);
+    (void)hipHostFree(mb_host);
+    mb_host = nullptr;
+    mb_dev = nullptr;
+    mb_stream = nullptr;
+    mailbox = false;
+  }
   void release_stream_resources() {
+    release_mailbox();
     if (small_done) (void)hipEventDestroy(small_done);
     small_done = nullptr;
     for (int b = 0; b < kRing; ++b) {
@@ -679,6 +744,27 @@ int eegfx_ctx_set_timing(eegfx_ctx* ctx, int enable) {
   });
 }
 
+int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    ctx->activate();
+    if (!enable) {
+      ctx->release_mailbox();
+      return;
+    }
+    if (ctx->mailbox) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&ctx->mb_stream, hipStreamNonBlocking));
+    HIP_CHECK(hipHostMalloc((void**)&ctx->mb_host, sizeof(MailboxCmd),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    memset(ctx->mb_host, 0, sizeof(MailboxCmd));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&ctx->mb_dev, ctx->mb_host, 0));
+    ctx->mb_seq = 0;
+    ctx->mb_launch();
+    ctx->mb_last = std::chrono::steady_clock::now();
+    ctx->mailbox = true;
+  });
+}
+
 int eegfx_ctx_synchronize(eegfx_ctx* ctx) {
   return guarded([&] {
     if (!ctx) fail(EEGFX_EINVAL, "null context");
@@ -735,6 +821,7 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    ctx->release_mailbox();  // before anything that synchronises the whole device
     (void)hipStreamSynchronize(ctx->stream);
     ctx->release_buffers();
     (void)hipStreamSynchronize(ctx->stream);
@@ -827,10 +914,20 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         // (features_small_kernel) reads them -- and writes the rows -- across the host link
         // directly: one launch and one stream sync, no DMA transfers (each costs a copy-engine
         // round trip) and no allocation once the context's staging has grown.
+        // growing a pinned buffer frees the old one, which synchronises the device: stop the
+        // resident server first (the next request restarts it)
+        if (ctx->mailbox && ((size_t)n * C * row_w > ctx->pin_in.cap || out_bytes > ctx->pin_out.cap))
+          ctx->mb_stop();
         double* hin = (double*)ctx->pin_in.get((size_t)n * C * row_w);
         double* hout = (double*)ctx->pin_out.get(out_bytes);
         for (int64_t r = 0; r < n * C; ++r)
           memcpy((uint8_t*)hin + (size_t)r * row_w, src + (size_t)r * row_p, row_w);
+        if (ctx->mailbox) {  // the resident server: no launch, no stream sync
+          (void)ctx->guard_for(n);
+          ctx->mb_serve(n, C, feature_size);
+          memcpy(out, hout, out_bytes);
+          return;
+        }
         ctx->tic();
         HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
                                         feature_size, ctx->numerics != EEGFX_EXACT,

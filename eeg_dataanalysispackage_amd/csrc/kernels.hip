@@ -777,20 +777,23 @@ static_assert(sizeof(double) * (kSmallMaxC * kWin + kSmallMaxC * 16 + 1) <= 160 
 // Under fma numerics the row is checked against the conditioning guard (guard.h, measured X per
 // channel); a failing row is recomputed right here with the EXACT cascade from the staged windows
 // (no follow-up launch on this latency-bound path), and counted in the guard's running total.
+struct SmallLds {
+  double xs[kSmallMaxC * kWin];
+  double feat[kSmallMaxC * 16];
+  double gx[kSmallMaxC];
+  double norm;
+  int redo;
+};
+
+// One epoch (its C x 512 window doubles at `src`, 16-byte aligned) -> its row at `dst`, by a
+// workgroup of 256 threads (uniform control flow; ends with a barrier).
 template <bool FAST>
-__global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
-                                                             int64_t n, int C, int nfeat,
-                                                             double* __restrict__ out,
-                                                             Guard guard) {
+__device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows, int C, int nfeat,
+                                            double* __restrict__ dst, const Guard& guard,
+                                            SmallLds& sh) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
-  __shared__ __attribute__((aligned(16))) double xs[kSmallMaxC * kWin];
-  __shared__ double feat[kSmallMaxC * 16];
-  __shared__ double gx[kSmallMaxC];
-  __shared__ double norm;
-  __shared__ int redo;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t e = blockIdx.x;
-  const f64x2* src = (const f64x2*)(rows + e * C * kWin);
+  const f64x2* src = (const f64x2*)src_rows;
   const int npairs = C * kWin / 2;  // <= 4096: at most 16 per thread
   f64x2 v[16];
 #pragma unroll
@@ -801,7 +804,7 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int i = tid + 256 * k;
-    if (i < npairs) *(f64x2*)(xs + 2 * i) = v[k];
+    if (i < npairs) *(f64x2*)(sh.xs + 2 * i) = v[k];
   }
   __syncthreads();
   const int F = C * nfeat;
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
     for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
       const int c = c0 + (lane >> 3);
       const bool valid = c < C;
-      const double* xr = xs + (valid ? c : 0) * kWin;
+      const double* xr = sh.xs + (valid ? c : 0) * kWin;
       double x[kIn];
 #pragma unroll
       for (int k = 0; k < kIn; ++k) x[k] = xr[(kSegLen * s + k) & (kWin - 1)];
@@ -822,11 +825,11 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
 #pragma unroll
         for (int k = 0; k < kSegLen; ++k) xm = fmax(xm, fabs(x[k]));
         xm = group8_max(xm);
-        if (valid && s == 0) gx[c] = xm * xm;
+        if (valid && s == 0) sh.gx[c] = xm * xm;
       }
       if (valid) {
-        if (s < nfeat) feat[c * nfeat + s] = a6;
-        if (8 + s < nfeat) feat[c * nfeat + 8 + s] = d6;
+        if (s < nfeat) sh.feat[c * nfeat + s] = a6;
+        if (8 + s < nfeat) sh.feat[c * nfeat + 8 + s] = d6;
       }
     }
     __syncthreads();
@@ -835,27 +838,90 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
   else bank(std::false_type{});
   if (tid == 0) {  // SignalProcessing.normalize: Math.pow(f, 2) summed in index order
     double acc = 0.0;
-    for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
-    norm = sqrt(acc);
-    redo = 0;
+    for (int i = 0; i < F; ++i) acc = acc + sh.feat[i] * sh.feat[i];
+    sh.norm = sqrt(acc);
+    sh.redo = 0;
     if (FAST && guard.total) {
       double sx = 0.0;
-      for (int c = 0; c < C; ++c) sx += gx[c];
-      redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
+      for (int c = 0; c < C; ++c) sx += sh.gx[c];
+      sh.redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
     }
   }
   __syncthreads();
-  if (FAST && redo) {  // uniform: the EXACT filter bank and normalisation on the staged windows
+  if (FAST && sh.redo) {  // uniform: the EXACT filter bank and normalisation on the staged windows
     bank(std::false_type{});
     if (tid == 0) {
       double acc = 0.0;
-      for (int i = 0; i < F; ++i) acc = acc + feat[i] * feat[i];
-      norm = sqrt(acc);
+      for (int i = 0; i < F; ++i) acc = acc + sh.feat[i] * sh.feat[i];
+      sh.norm = sqrt(acc);
       atomicAdd(guard.total, 1ull);
     }
     __syncthreads();
   }
-  for (int i = tid; i < F; i += 256) out[e * F + i] = feat[i] / norm;
+  for (int i = tid; i < F; i += 256) dst[i] = sh.feat[i] / sh.norm;
+  __syncthreads();  // sh is reused by the next epoch
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
+                                                             int64_t n, int C, int nfeat,
+                                                             double* __restrict__ out,
+                                                             Guard guard) {
+  __shared__ __attribute__((aligned(16))) SmallLds sh;
+  const int64_t e = blockIdx.x;
+  (void)n;
+  small_epoch<FAST>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, guard, sh);
+}
+
+// The opt-in resident form of the same path (eegfx_ctx_set_mailbox): one workgroup that stays on
+// the device and serves the context's small host batches without a launch each.  Thread 0 polls
+// the request word of a host-mapped MailboxCmd (system-scope atomic loads, a short s_sleep between
+// polls); a new request's epochs are read from its pinned rows, computed by small_epoch exactly as
+// features_small_kernel does, and written to its pinned output, then the completed sequence
+// number is published (system-scope release after every wave's stores).  The kernel returns when
+// the host sets `stop`, or after idle_ticks (s_memrealtime, 100 MHz) without a request -- every
+// wave reaches that exit; the host relaunches it on the next request.
+__global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, uint64_t idle_ticks,
+                                                               Guard guard) {
+  __shared__ __attribute__((aligned(16))) SmallLds sh;
+  __shared__ uint32_t cmd[2];  // request to serve, 0 = return
+  const int tid = threadIdx.x;
+  uint32_t last = __hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (tid == 0) {
+      uint32_t go = 0;
+      const uint64_t t0 = wall_clock64();
+      for (;;) {
+        const uint32_t r = __hip_atomic_load(&mb->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r != last) { go = r; break; }
+        if (__hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (wall_clock64() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      cmd[0] = go;
+    }
+    __syncthreads();
+    const uint32_t go = cmd[0];
+    if (go == 0) break;  // uniform: stop or idle
+    // every wave: no stale line of the (reused) pinned buffers from an earlier request
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const int64_t n = mb->n;
+    const int C = mb->C, nfeat = mb->nfeat;
+    const double* rows = mb->rows;
+    double* out = mb->out;
+    const int fast = mb->fast;
+    __syncthreads();  // every wave has read the command before the host may write the next
+    if (fast)
+      for (int64_t e = 0; e < n; ++e)
+        small_epoch<true>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, guard, sh);
+    else
+      for (int64_t e = 0; e < n; ++e)
+        small_epoch<false>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, Guard{nullptr, nullptr, nullptr}, sh);
+    __threadfence_system();  // this thread's rows reach the host before the flag below
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = go;
+  }
 }
 
 // ---- synthetic recordings ------------------------------------------------------
@@ -1029,6 +1095,9 @@ bool cut_features_supported(int fmt, int ct, int C, const void* raw, const doubl
                             const double* feat) {
   if (!(fmt == 0 || fmt == 1) || C < 1 || C > kMaxChannels || ct < 1) return false;
   if (((uintptr_t)raw & 3) || ((uintptr_t)out & 15) || !feat) return false;
+  // the 3-channel kernel stores its rows as 16-byte pairs (normalise_store); the staged kernels
+  // store doubles
+  if (fmt == 0 && ct == 3 && C == 3 && ((uintptr_t)feat & 15)) return false;
   const int fbytes = ct * (fmt == 0 ? 2 : 4);
   const size_t stage = fbytes % 4 != 0 ? (size_t)dev::kPost * fbytes + 8
                                        : (size_t)dev::kPost * ((fbytes / 4 + 1) * 4);
@@ -1060,6 +1129,12 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
 }
 
 bool features_small_supported(int C) { return C >= 1 && C <= dev::kSmallMaxC; }
+
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
+                                   const Guard& guard) {
+  hipLaunchKernelGGL(dev::features_mailbox_kernel, dim3(1), dim3(256), 0, st, mb, idle_ticks, guard);
+  return hipGetLastError();
+}
 
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
                                  bool fast, double* out, const Guard& guard) {

@@ -45,6 +45,20 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
 // one workgroup per epoch, C <= 16; rows / out may be device pointers of mapped pinned memory.
 bool features_small_supported(int C);
 // guard.total counts the rows the kernel recomputed under EXACT (guard.h); count/list unused.
+// The resident small-batch server (eegfx_ctx_set_mailbox): a host-mapped command block, written
+// by the host except `done` (the device's last completed request).
+struct MailboxCmd {
+  uint32_t req;   // request sequence number, incremented by the host after the fields below
+  uint32_t done;  // the last request whose rows are in `out` (device)
+  uint32_t stop;  // 1: the kernel returns
+  int32_t fast;   // numerics of the request (1 = EEGFX_FMA)
+  int64_t n;      // epochs
+  int32_t C, nfeat;
+  const double* rows;  // device-mapped pinned [n][C][512] window doubles
+  double* out;         // device-mapped pinned [n][C * nfeat] rows
+};
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
+                                   const Guard& guard);
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
                                  bool fast, double* out, const Guard& guard);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);

@@ -17,12 +17,19 @@
 //                         (FMA) before one coalesced store.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "dwt8.h"
 #include "guard.h"
 #include "launch.h"
 #include "lds_dma.h"
+
+// configs[3]'s 32-channel kernel as a persistent grid with the next window in flight
+// (window_c32_pp_kernel); 0 = one epoch per workgroup (window_c32_kernel)
+#ifndef EEGFX_C32_PP
+#define EEGFX_C32_PP 0
+#endif
 
 namespace eegfx {
 namespace dev {
@@ -296,51 +303,53 @@ __global__ __launch_bounds__(256) void window_wide_kernel(
 }
 
 // configs[3]: the full 32-channel int16 montage with every channel through the DWT (512-dim rows),
-// one epoch per workgroup of 4 waves (wave w = channels 8w..8w+7, lane = (channel, segment)).
-// Everything the generic kernel computes from runtime sizes is constexpr here: the staging rows
-// (wave w issues rows w, w+4, ...; scalar row bases, two VALU instructions of lane offset per row,
-// no per-lane bounds test when the window lies inside the recording), the signal -> channel map
-// (shifts) and the row normalisation (FMA: rsqrt_nr, one multiply per feature; EXACT keeps the
-// reference's sequential sum and division).  Measured against the
-// generic kernel at FB = 64 (tools/probes, 666 launches of 250k epochs): 2.58 -> 2.46 ms,
-// 1,114 -> 1,040 VALU instructions per wave.
-template <bool FAST, bool STREAM>
-__global__ __launch_bounds__(256) void window_c32_kernel(
-    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
-    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
-    double* __restrict__ out, Guard guard) {
-  constexpr int C = 32, FB = 64, SEGQ = 4 * FB + 1, EQ = 8 * SEGQ, F = 16 * C;
-  constexpr int NROWS = (EQ + 63) / 64;  // 33
-  __shared__ __attribute__((aligned(16))) uint8_t win[EQ * 16];
-  __shared__ __attribute__((aligned(16))) double feat[F];
-  __shared__ double norm1;
-  __shared__ double gx[FAST ? C : 1];  // the guard's X^2 per channel (fma numerics)
-  __shared__ int redo;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t nbytes = n_frames * FB;
+// one epoch at a time per workgroup of 4 waves (wave w = channels 8w..8w+7, lane = (channel,
+// segment)).  Everything the generic kernel computes from runtime sizes is constexpr here: the
+// staging rows (wave w issues rows w, w+4, ...; scalar row bases, two VALU instructions of lane
+// offset per row, no per-lane bounds test when the window lies inside the recording), the signal
+// -> channel map (shifts) and the row normalisation (FMA: rsqrt_nr, one multiply per feature;
+// EXACT keeps the reference's sequential sum and division).  Measured against the generic kernel
+// at FB = 64 (tools/probes, 666 launches of 250k epochs): 2.58 -> 2.46 ms, 1,114 -> 1,040 VALU
+// instructions per wave.
+struct C32 {
+  static constexpr int C = 32, FB = 64, SEGQ = 4 * FB + 1, EQ = 8 * SEGQ, F = 16 * C;
+  static constexpr int NROWS = (EQ + 63) / 64;  // 33
+  static constexpr int64_t SPAN = (int64_t)64 * FB * 7 + 16 * SEGQ;
+};
+
+// Byte offset of epoch e's window (an invalid position, flagged by the baselines, is cut as 100).
+__device__ __forceinline__ int64_t c32_window(const int64_t* __restrict__ pos, int64_t e,
+                                              int64_t n_frames) {
   const int64_t p0 = pos[e];
-  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : (int64_t)kPre;  // flagged by baselines
-  const int64_t B = (p + 175) * FB;
+  const int64_t p = p0 >= kPre && p0 - kPre <= n_frames ? p0 : (int64_t)kPre;
+  return (p + 175) * C32::FB;
+}
+
+// Stages the window at byte B into `win` (this wave's rows).  Row j = w + 4t holds LDS quads
+// i = 64 j + lane; quad i = SEGQ sg + rem lands from byte 4096 sg + 16 rem = 16 i - 16 sg of the
+// window.  A row spans 64 < SEGQ quads, so it crosses at most one segment boundary: sg = s0 +
+// [lane >= t_j] with s0 = floor(64 j / SEGQ), and the offset splits into a scalar row base
+// (1024 j - 16 s0) and a per-lane 16 lane - 16 [lane >= t_j] (two VALU instructions per row).
+// Returns whether the whole window lay inside the recording (every row one LDS-DMA, 9 for wave 0
+// and 8 for the others, tracked by vmcnt); otherwise the quads past either end were filled
+// directly.
+template <bool STREAM>
+__device__ __forceinline__ bool c32_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
+                                          int64_t B, uint8_t* win, int w, int lane) {
+  using K = C32;
   const int64_t Bq = B & ~(int64_t)15;
-  constexpr int64_t span = (int64_t)64 * FB * 7 + 16 * SEGQ;
-  const bool full = Bq >= 0 && Bq + span <= nbytes;
-  // Row j = w + 4t holds LDS quads i = 64 j + lane; quad i = SEGQ sg + rem lands from byte
-  // 4096 sg + 16 rem = 16 i - 16 sg of the window.  A row spans 64 < SEGQ quads, so it crosses at
-  // most one segment boundary: sg = s0 + [lane >= t_j] with s0 = floor(64 j / SEGQ), and the
-  // offset splits into a scalar row base (1024 j - 16 s0) and a per-lane 16 lane - 16 [lane >= t_j]
-  // (two VALU instructions per row).
+  const bool full = Bq >= 0 && Bq + K::SPAN <= nbytes;
   const uint32_t lane16 = 16u * (uint32_t)lane;
 #pragma unroll
-  for (int t = 0; t < (NROWS + 3) / 4; ++t) {
+  for (int t = 0; t < (K::NROWS + 3) / 4; ++t) {
     const int j = w + 4 * t;
-    if (j < NROWS) {  // uniform
-      const int s0 = (64 * j) / SEGQ;
-      const int tj = SEGQ * (s0 + 1) - 64 * j;
+    if (j < K::NROWS) {  // uniform
+      const int s0 = (64 * j) / K::SEGQ;
+      const int tj = K::SEGQ * (s0 + 1) - 64 * j;
       const uint32_t voff = lane16 - (lane >= tj ? 16u : 0u);
       const int64_t rowb = 1024 * (int64_t)j - 16 * (int64_t)s0;
       uint8_t* dst = win + (size_t)(64 * j) * 16;
-      const bool lane_in = 64 * j + 64 <= EQ || 64 * j + lane < EQ;
+      const bool lane_in = 64 * j + 64 <= K::EQ || 64 * j + lane < K::EQ;
       if (full) {  // uniform: the whole window lies inside the recording
         if (lane_in) dma16_s<STREAM>(raw + Bq + rowb, voff, dst);
       } else if (lane_in) {
@@ -355,15 +364,33 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
       }
     }
   }
-  dma_drain();
-  __syncthreads();
+  return full;
+}
 
+// LDS of a 32-channel workgroup beside its window buffer(s).
+struct C32Shared {
+  double feat[C32::F];
+  double norm1;
+  double gx[C32::C];  // the guard's X^2 per channel (fma numerics)
+  int redo;
+};
+
+// Filter bank, normalisation and store of epoch e from its staged window (published by a
+// barrier); b = this lane's baseline.  Ends with every wave done reading `win` and sh.feat.
+template <bool FAST, bool STREAM>
+__device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int64_t n_frames,
+                                            const ChanSel& sel, const float* __restrict__ base,
+                                            int64_t e, int64_t B, float b, uint8_t* win,
+                                            C32Shared& sh, double* __restrict__ out,
+                                            const Guard& guard, int tid) {
+  using K = C32;
+  constexpr int C = K::C, FB = K::FB, SEGQ = K::SEGQ, F = K::F;
+  const int lane = tid & 63, w = tid >> 6;
   const int c = w * 8 + (lane >> 3), s = lane & 7;
   const uint8_t* eb = win + (int)(B & 15) + sel.col[c] * 2;
   const uint8_t* own = eb + 16 * SEGQ * s;
   const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
   const float r = sel.res[c];
-  const float b = base[e * C + c];
   double a6, d6;
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
@@ -380,9 +407,10 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
     halo<32, true>(a1, nullptr, lane & ~7, s);
     dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
   }
+  double* feat = sh.feat;
   feat[c * 16 + s] = a6;
   feat[c * 16 + 8 + s] = d6;
-  if (FAST && EEGFX_GUARD && s == 0) gx[c] = guard_x2_int16(r, b);
+  if (FAST && EEGFX_GUARD && s == 0) sh.gx[c] = guard_x2_int16(r, b);
   __syncthreads();
   double* o = out + e * F;
   if constexpr (FAST) {
@@ -390,7 +418,7 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
       double acc = 0.0;
 #pragma unroll
       for (int k = 0; k < F / 64; ++k) acc = __builtin_fma(feat[lane + 64 * k], feat[lane + 64 * k], acc);
-      double sx = lane < C ? gx[lane] : 0.0;
+      double sx = lane < C ? sh.gx[lane] : 0.0;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
         acc += __shfl_xor(acc, off, 64);
@@ -414,16 +442,17 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
                 C, lane));
       }
       if (lane == 0) {
-        norm1 = rsqrt_nr(acc);
-        redo = fails;
+        sh.norm1 = rsqrt_nr(acc);
+        sh.redo = fails;
       }
     }
     __syncthreads();
-    if (redo) {  // the guard's rare path: wave 0 recomputes the row under EXACT (window LDS free)
+    if (sh.redo) {  // the guard's rare path: wave 0 recomputes the row under EXACT (window LDS free)
       if (w == 0) {
+        const int64_t f0 = B / FB;
         dwt8_exact_row_wave(
             [&](int cc, int k) {
-              const float v = p + 175 + k < n_frames
+              const float v = f0 + k < n_frames
                                   ? (float)*(const int16_t*)(raw + B + (int64_t)k * FB + 2 * sel.col[cc])
                                   : 0.0f;
               float y = v * sel.res[cc];
@@ -432,13 +461,13 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
             },
             C, 16, (double*)win, feat, lane);
         if (lane == 0) {
-          norm1 = 1.0;  // the row is normalised
+          sh.norm1 = 1.0;  // the row is normalised
           atomicAdd(guard.total, 1ull);
         }
       }
       __syncthreads();
     }
-    const double inv = norm1;
+    const double inv = sh.norm1;
     typedef double f64x2 __attribute__((ext_vector_type(2)));
     const f64x2 v = *(const f64x2*)(feat + 2 * tid);
     const f64x2 q = {v.x * inv, v.y * inv};
@@ -448,15 +477,72 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
     if (tid == 0) {
       double acc = 0.0;
       for (int k = 0; k < F; ++k) acc = acc + feat[k] * feat[k];
-      norm1 = sqrt(acc);
+      sh.norm1 = sqrt(acc);
     }
     __syncthreads();
-    const double nv = norm1;
+    const double nv = sh.norm1;
     for (int k = tid; k < F; k += 256) {
       const double v = feat[k] / nv;
       if constexpr (STREAM) __builtin_nontemporal_store(v, o + k);
       else o[k] = v;
     }
+  }
+}
+
+template <bool FAST, bool STREAM>
+__global__ __launch_bounds__(256) void window_c32_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
+    double* __restrict__ out, Guard guard) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[C32::EQ * 16];
+  __shared__ C32Shared sh;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t B = c32_window(pos, e, n_frames);
+  (void)c32_issue<STREAM>(raw, n_frames * C32::FB, B, win, w, lane);
+  const float b = base[e * C32::C + w * 8 + (lane >> 3)];
+  dma_drain();
+  __syncthreads();
+  c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, win, sh, out, guard, tid);
+}
+
+// The same epochs with the next window in flight: a persistent grid (two workgroups per CU, two
+// window buffers each, 70 KB) walks a contiguous range of epochs per workgroup; epoch e+1's window
+// DMA leaves before epoch e's filter bank starts, and only e's DMAs are waited for (vmcnt = the
+// rows in flight).  A window that crosses either end of the recording drains everything.
+template <bool FAST, bool STREAM>
+__global__ __launch_bounds__(256) void window_c32_pp_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
+    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
+    double* __restrict__ out, Guard guard) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[2][C32::EQ * 16];
+  __shared__ C32Shared sh;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t nbytes = n_frames * C32::FB;
+  const int64_t G = gridDim.x, g = blockIdx.x;
+  const int64_t e_begin = g * n / G, e_end = (g + 1) * n / G;
+  if (e_begin >= e_end) return;  // uniform per workgroup
+  int64_t B = c32_window(pos, e_begin, n_frames);
+  bool full = c32_issue<STREAM>(raw, nbytes, B, win[0], w, lane);
+  int64_t B_next = e_begin + 1 < e_end ? c32_window(pos, e_begin + 1, n_frames) : 0;
+  for (int64_t e = e_begin; e < e_end; ++e) {
+    const int cur = (int)((e - e_begin) & 1);
+    // loads of this epoch and of the window after next, before the next DMAs leave (vmcnt below
+    // then waits for nothing issued after them)
+    const float b = base[e * C32::C + w * 8 + (lane >> 3)];
+    const int64_t B_after = e + 2 < e_end ? c32_window(pos, e + 2, n_frames) : 0;
+    bool full_next = true;
+    const bool more = e + 1 < e_end;
+    if (more) full_next = c32_issue<STREAM>(raw, nbytes, B_next, win[cur ^ 1], w, lane);
+    if (!more || !full || !full_next) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (w == 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __syncthreads();  // epoch e's window is visible to every wave
+    c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, win[cur], sh, out, guard, tid);
+    __syncthreads();  // every wave is done with win[cur] and sh before they are reused
+    B = B_next;
+    B_next = B_after;
+    full = full_next;
   }
 }
 
@@ -558,10 +644,17 @@ static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, in
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard);
   if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) {  // configs[3]
     const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
+#if EEGFX_C32_PP
+    const dim3 g((unsigned)std::min<int64_t>(n, 2 * 256));  // two resident workgroups per CU
+#define EEGFX_C32(FA, NTV) \
+    hipLaunchKernelGGL((dev::window_c32_pp_kernel<FA, NTV>), g, dim3(256), 0, st, \
+                       (const uint8_t*)raw, n_frames, sel, pos, base, n, out, guard)
+#else
     const dim3 g((unsigned)n);
 #define EEGFX_C32(FA, NTV) \
     hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV>), g, dim3(256), 0, st, (const uint8_t*)raw, \
                        n_frames, sel, pos, base, n, out, guard)
+#endif
     if (fast) { if (nt) EEGFX_C32(true, true); else EEGFX_C32(true, false); }
     else { if (nt) EEGFX_C32(false, true); else EEGFX_C32(false, false); }
 #undef EEGFX_C32

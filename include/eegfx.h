@@ -122,6 +122,15 @@ int eegfx_ctx_guard_stats(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_r
  * NULL. */
 int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_rechecked,
                            int64_t* rows_recomputed, int reset);
+/* Opt-in resident server for the per-epoch drop-in (IFeatureExtraction.extractFeatures called
+ * once per epoch, LogisticRegressionClassifier.java:55-61): enable != 0 starts one resident
+ * workgroup on its own stream that polls a host-mapped command word, so small EEGFX_MEM_HOST
+ * eegfx_extract_features_f64 batches on this context (<= 768 KB of window rows, C <= 16) are
+ * served without a kernel launch or a stream synchronisation -- the same kernel code, the same
+ * rows.  It returns by itself after 1 s without a request (and is restarted by the next one), or
+ * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
+ * (hipDeviceSynchronize) waits for it: disable it before such calls.  Off by default. */
+int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
 /* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */

@@ -61,6 +61,32 @@ def test_recordings_one_pass(ctx, ctx_fma, base, guessed):
     assert eq(ep, want_ep) and within(f, want_f)
 
 
+@pytest.mark.parametrize("numerics", ["exact", "fma"])
+def test_unaligned_device_features_take_the_two_pass_route(ctx, ctx_fma, numerics):
+    """A device `features` view offset by one double (8-byte aligned): the 3-channel one-pass
+    kernel stores 16-byte row pairs, so such a pointer takes the cut + batch-extract route
+     -- same rows, no misaligned vector stores."""
+    import torch
+    raw = fx.read_raw(DOD02 + ".vhdr", DOD02 + ".eeg")
+    allpos = [m.position for m in fx.read_markers(DOD02 + ".vmrk") if m.position >= 100]
+    n = len(allpos)
+    c = ctx if numerics == "exact" else ctx_fma
+    want_f = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, allpos)
+    want_ep = oracle.decode_epochs(raw, [0, 1, 2], [0.1] * 3, allpos)
+    buf = torch.full((n * 48 + 1,), float("nan"), dtype=torch.float64, device="cuda")
+    feats = buf[1:].view(n, 48)
+    assert feats.data_ptr() % 16 == 8
+    ep = torch.empty((n, 3, 750), dtype=torch.float64, device="cuda")
+    c.process_recording_epochs(torch.from_numpy(raw).cuda(), 3, [0, 1, 2], [0.1] * 3,
+                               torch.from_numpy(np.asarray(allpos, dtype=np.int64)).cuda(),
+                               out=feats, epochs_out=ep)
+    c.synchronize()
+    assert eq(ep.cpu().numpy(), want_ep)
+    got = feats.cpu().numpy()
+    assert eq(got, want_f) if numerics == "exact" else within(got, want_f)
+    assert torch.isnan(buf[0])
+
+
 LAYOUTS = [  # (ct, cols, fmt)
     (3, [0, 1, 2], np.int16),          # the reference's Fz/Cz/Pz file: 6-byte packed frames
     (5, [4, 1], np.int16),             # packed, 2 of 5 channels

@@ -1,0 +1,94 @@
+"""The opt-in resident server of the per-epoch drop-in (eegfx_ctx_set_mailbox): small host
+extract batches -- IFeatureExtraction.extractFeatures called once per epoch from the Spark map
+closure (LogisticRegressionClassifier.java:55-61) -- served by a workgroup that stays on the
+device.  Bar: the same rows as the launch path (the same kernel code), bit for bit, in both
+numerics; the server survives buffer growth, its own idle exit, concurrent contexts and a
+context destroyed with it running.  Every context here is host-only (no torch device sync while a
+server is resident)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import eeg_dataanalysispackage_amd as fx
+from conftest import INFO_TRAIN, hexrows
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def eq(a, b):
+    return np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.fixture(scope="module")
+def epochs():
+    odp = fx.OffLineDataProvider([INFO_TRAIN])
+    odp.loadData()
+    return np.ascontiguousarray(odp.getData())
+
+
+@pytest.mark.parametrize("numerics", ["exact", "fma"])
+def test_mailbox_rows_equal_launch_path(epochs, golden_vectors, numerics):
+    c = fx.Context(0, numerics=numerics)
+    try:
+        want = np.stack([c.extract_features(epochs[i:i + 1])[0] for i in range(len(epochs))])
+        c.set_mailbox(True)
+        got = np.stack([c.extract_features(epochs[i:i + 1])[0] for i in range(len(epochs))])
+        assert eq(got, want)
+        assert eq(c.extract_features(epochs), want)                 # the 11-epoch batch
+        if numerics == "exact":
+            assert eq(got, hexrows(golden_vectors["infoTrain"]["features_hex"]))
+        # growth of the pinned staging (stops and restarts the server), then small again
+        big = np.concatenate([epochs] * 6)                          # 66 epochs, 1.6 MB rows
+        assert eq(c.extract_features(big[:64]), np.concatenate([want] * 6)[:64])
+        assert eq(c.extract_features(epochs[3:4]), want[3:4])
+        c.set_mailbox(False)
+        assert eq(c.extract_features(epochs[5:6]), want[5:6])       # back on the launch path
+    finally:
+        c.set_mailbox(False)
+        c.close()
+
+
+def test_mailbox_idle_exit_and_restart(epochs):
+    c = fx.Context(0)
+    try:
+        want = oracle.extract_features(epochs[:2])
+        c.set_mailbox(True)
+        assert eq(c.extract_features(epochs[:1]), want[:1])
+        time.sleep(1.3)   # longer than the server's 1 s idle limit: it has returned
+        assert eq(c.extract_features(epochs[1:2]), want[1:2])
+        c.set_mailbox(True)   # idempotent
+        assert eq(c.extract_features(epochs[:2]), want)
+    finally:
+        c.set_mailbox(False)
+        c.close()
+
+
+def test_mailbox_concurrent_contexts_and_destroy(epochs):
+    """Four threads, a context and a resident server each (the Spark executor threads), all
+    serving single epochs at once; every context destroyed with its server still running."""
+    want = oracle.extract_features(epochs)
+    errors = []
+
+    def work(t):
+        c = fx.Context(0)
+        try:
+            c.set_mailbox(True)
+            for k in range(200):
+                i = (t + k) % len(epochs)
+                if not eq(c.extract_features(epochs[i:i + 1]), want[i:i + 1]):
+                    errors.append((t, k))
+        except Exception as exc:   # reported below
+            errors.append(repr(exc))
+        finally:
+            c.close()              # destroys the context with the server resident
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=90)
+    assert not any(x.is_alive() for x in th)
+    assert errors == []

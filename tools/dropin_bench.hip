@@ -13,7 +13,10 @@
 //            one thread -- the per-thread rate of the CPU baseline; beside it the optimised CPU
 //            form (oracle_extract_features_fast: minimal cascade, channels in AVX2 lanes);
 //   sync     the floor of one launch round trip on this box: an empty kernel + hipStreamSynchronize,
-//            and the same with a spin on hipEventQuery.
+//            and the same with a spin on hipEventQuery;
+//   mailbox  the same calls served by the context's resident workgroup (eegfx_ctx_set_mailbox):
+//            one epoch per call, the 11-epoch batch, and T threads with a server each; every row
+//            compared bit for bit with the launch path's.
 // Prints one JSON object.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -56,6 +59,7 @@ struct Job {
   int reps;
   double per_call;
   int rc;
+  int mailbox;
 };
 static void* worker(void* arg) {
   Job* j = (Job*)arg;
@@ -63,6 +67,7 @@ static void* worker(void* arg) {
   j->rc = eegfx_ctx_create(0, &ctx);
   if (j->rc) return nullptr;
   eegfx_ctx_set_numerics(ctx, g_numerics);
+  if (j->mailbox) j->rc |= eegfx_ctx_set_mailbox(ctx, 1);
   double out[48];
   for (int i = 0; i < 20; ++i)
     eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out, EEGFX_MEM_HOST);
@@ -164,7 +169,7 @@ int main(int argc, char** argv) {
   for (int ti = 0; ti < 3; ++ti) {
     const int T = Ts[ti];
     std::vector<pthread_t> th((size_t)T);
-    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0});
+    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 0});
     for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
     double agg = 0, mean = 0;
     int rc = 0;
@@ -178,6 +183,65 @@ int main(int argc, char** argv) {
            ti ? ", " : "", T, 1.0 / mean, agg, rc);
   }
   printf("},\n");
+
+  // the resident server: the same calls without a launch each, rows compared with the launch path
+  {
+    std::vector<double> want((size_t)k * 48), got((size_t)k * 48);
+    for (int64_t i = 0; i < k; ++i)
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)i * 2250, 1, 3, 8, 512, 175, 16,
+                                    want.data() + i * 48, EEGFX_MEM_HOST));
+    CK(eegfx_ctx_set_mailbox(ctx, 1));
+    for (int i = 0; i < 200; ++i)
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                    EEGFX_MEM_HOST));
+    lat.clear();
+    for (int i = 0; i < reps; ++i) {
+      const double t0 = now_s();
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)(i % k) * 2250, 1, 3, 8, 512,
+                                    175, 16, got.data() + (i % k) * 48, EEGFX_MEM_HOST));
+      lat.push_back(now_s() - t0);
+    }
+    const Lat mb = stats(lat);
+    bool same = std::equal(want.begin(), want.end(), got.begin(), [](double a, double b) {
+      return a == b || (a != a && b != b);
+    });
+    std::vector<double> got11((size_t)k * 48);
+    lat.clear();
+    for (int i = 0; i < reps / 4; ++i) {
+      const double t0 = now_s();
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data(), k, 3, 8, 512, 175, 16, got11.data(),
+                                    EEGFX_MEM_HOST));
+      lat.push_back(now_s() - t0);
+    }
+    const Lat mb11 = stats(lat);
+    same = same && std::equal(want.begin(), want.end(), got11.begin(), [](double a, double b) {
+      return a == b || (a != a && b != b);
+    });
+    CK(eegfx_ctx_set_mailbox(ctx, 0));
+    printf(" \"mailbox\": {\"single_epoch\": {\"median_us\": %.2f, \"p99_us\": %.2f, "
+           "\"epochs_per_s\": %.1f}, \"batch_11\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f}, "
+           "\"rows_identical_to_launch_path\": %s, \"threads\": {",
+           mb.med * 1e6, mb.p99 * 1e6, 1.0 / mb.med, mb11.med * 1e6, k / mb11.med,
+           same ? "true" : "false");
+    const int Tm[3] = {2, 4, 8};
+    for (int ti = 0; ti < 3; ++ti) {
+      const int T = Tm[ti];
+      std::vector<pthread_t> th((size_t)T);
+      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1});
+      for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
+      double agg = 0, mean = 0;
+      int rc = 0;
+      for (int t = 0; t < T; ++t) {
+        pthread_join(th[(size_t)t], nullptr);
+        agg += 1.0 / jobs[(size_t)t].per_call;
+        mean += jobs[(size_t)t].per_call / T;
+        rc |= jobs[(size_t)t].rc;
+      }
+      printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, \"rc\": %d}",
+             ti ? ", " : "", T, 1.0 / mean, agg, rc);
+    }
+    printf("}},\n");
+  }
 
   // the C port, one thread
   void* h = dlopen((repo + "/oracle/liboracle.so").c_str(), RTLD_NOW);

@@ -1,14 +1,19 @@
 # (1) GPU tests of this round's changes: the guard's second stage (every int16 fma kernel), the
-#     mini-batch logistic regression, the Java shim's call sequence from C;
+#     mini-batch logistic regression, the Java shim's call sequence from C, the resident
+#     per-epoch server, the unaligned-features route;
 # (2) the guard's flag-rate study on the fast second stage (--plant flat / null);
-# (3) window kernel with 1, 2, 3 sub-tiles per workgroup (EEGFX_WIN_SUBS, probes wp_s1..3):
-#     window and step, interleaved, three repetitions.
+# (3) window kernel with 1, 2, 3 sub-tiles per workgroup (EEGFX_WIN_SUBS, probes wp_s1..3) and
+#     the 32-channel kernel one-epoch-per-workgroup vs persistent ping-pong (wp_c32base /
+#     wp_c32pp), interleaved, three repetitions;
+# (4) the per-epoch drop-in with and without the resident server (tools/dropin_bench).
 set -uo pipefail
-OUT=gpurun_out/r05c
+OUT=gpurun_out/r05d
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_guard.py tests/test_gpu_logreg.py tests/test_gpu_c_abi.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_mailbox.py tests/test_gpu_guard.py tests/test_gpu_logreg.py tests/test_gpu_c_abi.py tests/test_gpu_epochs_features.py -x -q --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
+timeout -k 10 300 ./tools/dropin_bench . 3000 1 > $OUT/dropin.json 2> $OUT/dropin.err || { tail -20 $OUT/dropin.err; exit 1; }
+cat $OUT/dropin.json
 B="--cpu-sample 0 --alt-steps 0 --steps 50 --warmup 20"
 for spec in none flat:0.01 flat:0.1 flat:0.32 flat:1.0 null:0.01 null:0.1 null:0.32; do
   if [ $spec = none ]; then PL=""; else PL="--plant $spec"; fi
@@ -26,5 +31,9 @@ for rep in 1 2 3; do
     timeout -k 10 60 $P/$v >> $OUT/subs_window.log 2>&1 || { echo "$v failed"; tail -3 $OUT/subs_window.log; exit 1; }
     PROBE_STEP=1 timeout -k 10 60 $P/$v >> $OUT/subs_step.log 2>&1 || { echo "$v step failed"; exit 1; }
   done
+  for v in wp_c32base wp_c32pp; do
+    PROBE_WIDE=1 PROBE_ITERS=1000 timeout -k 10 60 $P/$v >> $OUT/c32_window.log 2>&1 || { echo "$v failed"; tail -3 $OUT/c32_window.log; exit 1; }
+  done
 done
 echo "== window (s1 s2 s3 x3)"; cat $OUT/subs_window.log; echo "== step"; cat $OUT/subs_step.log
+echo "== c32 (base pp x3)"; cat $OUT/c32_window.log
