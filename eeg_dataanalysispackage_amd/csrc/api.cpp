@@ -8,9 +8,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <thread>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -218,6 +221,9 @@ struct eegfx_ctx {
   std::chrono::steady_clock::time_point mb_last{};
   static constexpr uint64_t kMbIdleTicks = 100000000;  // 1 s of s_memrealtime (100 MHz)
   void mb_launch() {
+    // the staging a server reads is fixed for its lifetime (growing it stops the server first)
+    mb_host->rows = pin_in.p ? (const double*)pin_in.device_ptr() : nullptr;
+    mb_host->out = pin_out.p ? (double*)pin_out.device_ptr() : nullptr;
     const Guard g{guard_dev, nullptr, (unsigned long long*)(guard_dev + 2),
                   (unsigned long long*)(guard_dev + 4)};
     HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks, g));
@@ -226,32 +232,43 @@ struct eegfx_ctx {
   void mb_stop() {
     if (!mb_host) return;
     __atomic_store_n(&mb_host->stop, 1u, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(mb_stream);  // the kernel sees `stop` within one poll
+    // the kernel sees `stop` within one poll; a server that does not return is reported, not
+    // waited on forever
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipStreamQuery(mb_stream)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+        mb_live = false;
+        fail(EEGFX_EHIP, "mailbox server did not stop within 10 s");
+      }
+      std::this_thread::yield();
+    }
     __atomic_store_n(&mb_host->stop, 0u, __ATOMIC_RELEASE);
     mb_live = false;
+    HIP_CHECK(q);
+  }
+  // hipSuccess: the server kernel has returned; hipErrorNotReady: it is running; anything else
+  // is an error of the stream and is raised
+  bool mb_returned() {
+    const hipError_t q = hipStreamQuery(mb_stream);
+    if (q == hipErrorNotReady) return false;
+    HIP_CHECK(q);
+    return true;
   }
   // One request: n epochs of packed window rows in pin_in -> rows in pin_out.
   void mb_serve(int64_t n, int C, int nfeat) {
     MailboxCmd* m = mb_host;
-    m->n = n;
-    m->C = C;
-    m->nfeat = nfeat;
-    m->fast = numerics != EEGFX_EXACT ? 1 : 0;
-    m->rows = (const double*)pin_in.device_ptr();
-    m->out = (double*)pin_out.device_ptr();
     if (++mb_seq == 0) mb_seq = 1;  // 0 means "no request" to the kernel
     const auto now = std::chrono::steady_clock::now();
     // the kernel returns after 1 s without a request: relaunch it when it may have
-    if (!mb_live ||
-        (now - mb_last > std::chrono::milliseconds(500) && hipStreamQuery(mb_stream) == hipSuccess))
-      mb_launch();
-    __atomic_store_n(&m->req, mb_seq, __ATOMIC_RELEASE);
+    if (!mb_live || (now - mb_last > std::chrono::milliseconds(500) && mb_returned())) mb_launch();
+    __atomic_store_n(&m->req, mailbox_request(mb_seq, numerics != EEGFX_EXACT, C, nfeat, n),
+                     __ATOMIC_RELEASE);
     for (uint64_t spin = 1;; ++spin) {
       if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == mb_seq) break;
       if ((spin & 4095) == 0) {
         // the kernel went idle between the check above and the request: serve it again
-        if (hipStreamQuery(mb_stream) == hipSuccess &&
-            __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != mb_seq)
+        if (mb_returned() && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != mb_seq)
           mb_launch();
         if (std::chrono::steady_clock::now() - now > std::chrono::seconds(30))
           fail(EEGFX_EHIP, "mailbox request %u not served within 30 s", mb_seq);

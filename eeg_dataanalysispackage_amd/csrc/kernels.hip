@@ -785,6 +785,14 @@ struct SmallLds {
   int redo;
 };
 
+// lane j's v (j wave-uniform), as a wave-uniform value
+__device__ __forceinline__ double lane_value(double v, int j) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
 // One epoch (its C x 512 window doubles at `src`, 16-byte aligned) -> its row at `dst`, by a
 // workgroup of 256 threads (uniform control flow; ends with a barrier).
 template <bool FAST>
@@ -836,25 +844,40 @@ __device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows,
   };
   if constexpr (FAST) bank(std::true_type{});
   else bank(std::false_type{});
-  if (tid == 0) {  // SignalProcessing.normalize: Math.pow(f, 2) summed in index order
+  // SignalProcessing.normalize: Math.pow(f, 2) summed in index order.  Wave 0 squares 64
+  // features at a time, one per lane, and the running sum walks the lanes in order (readlane),
+  // so the additions are the reference's, in its order, without a serial LDS round trip each.
+  auto sum_squares = [&]() {
     double acc = 0.0;
-    for (int i = 0; i < F; ++i) acc = acc + sh.feat[i] * sh.feat[i];
-    sh.norm = sqrt(acc);
-    sh.redo = 0;
-    if (FAST && guard.total) {
-      double sx = 0.0;
-      for (int c = 0; c < C; ++c) sx += sh.gx[c];
-      sh.redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
+    for (int base = 0; base < F; base += 64) {
+      const int i = base + lane;
+      const double sq = i < F ? sh.feat[i] * sh.feat[i] : 0.0;
+      const int m = F - base < 64 ? F - base : 64;
+      for (int j = 0; j < m; ++j) acc = acc + lane_value(sq, j);
+    }
+    return acc;
+  };
+  if (w == 0) {  // uniform per wave
+    const double acc = sum_squares();
+    if (lane == 0) {
+      sh.norm = sqrt(acc);
+      sh.redo = 0;
+      if (FAST && guard.total) {
+        double sx = 0.0;
+        for (int c = 0; c < C; ++c) sx += sh.gx[c];
+        sh.redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
+      }
     }
   }
   __syncthreads();
   if (FAST && sh.redo) {  // uniform: the EXACT filter bank and normalisation on the staged windows
     bank(std::false_type{});
-    if (tid == 0) {
-      double acc = 0.0;
-      for (int i = 0; i < F; ++i) acc = acc + sh.feat[i] * sh.feat[i];
-      sh.norm = sqrt(acc);
-      atomicAdd(guard.total, 1ull);
+    if (w == 0) {
+      const double acc = sum_squares();
+      if (lane == 0) {
+        sh.norm = sqrt(acc);
+        atomicAdd(guard.total, 1ull);
+      }
     }
     __syncthreads();
   }
@@ -886,41 +909,59 @@ __global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, u
   __shared__ __attribute__((aligned(16))) SmallLds sh;
   __shared__ uint32_t cmd[2];  // request to serve, 0 = return
   const int tid = threadIdx.x;
-  uint32_t last = __hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // Control flow stays wave-uniform throughout: wave 0 polls with all 64 lanes (one request per
+  // poll, the loaded word made uniform with readfirstlane).  A lane-divergent `if (tid == 0)`
+  // poll at the loop top let the compiler structurise the loop so that lanes other than 0 went
+  // round the served request again instead of waiting at the barrier -- the server then never
+  // answered.
+  const bool wave0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
+  uint32_t last = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)__hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+  const double* rows = mb->rows;
+  double* out = mb->out;
   for (;;) {
-    if (tid == 0) {
-      uint32_t go = 0;
+    if (wave0) {
+      uint64_t go = 0;
       const uint64_t t0 = wall_clock64();
       for (;;) {
-        const uint32_t r = __hip_atomic_load(&mb->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (r != last) { go = r; break; }
-        if (__hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        const uint64_t r = __hip_atomic_load(&mb->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(r >> 32));
+        if (hi != last) {
+          go = (uint64_t)hi << 32 | lo;
+          break;
+        }
+        if (__builtin_amdgcn_readfirstlane(
+                (int)__hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)))
+          break;
         if (wall_clock64() - t0 > idle_ticks) break;
         __builtin_amdgcn_s_sleep(2);
       }
-      cmd[0] = go;
+      if (tid == 0) {
+        cmd[0] = (uint32_t)(go >> 32);
+        cmd[1] = (uint32_t)go;
+      }
     }
     __syncthreads();
-    const uint32_t go = cmd[0];
-    if (go == 0) break;  // uniform: stop or idle
-    // every wave: no stale line of the (reused) pinned buffers from an earlier request
+    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)cmd[0]);
+    if (seq == 0) break;  // stop or idle
+    const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane((int)cmd[1]);
+    const int fast = (int)(word >> 31);
+    const int C = (int)((word >> 26) & 31) + 1, nfeat = (int)((word >> 21) & 31) + 1;
+    const int64_t n = (int64_t)(word & ((1u << 21) - 1));
+    // every wave: no stale line of the (reused) pinned rows from an earlier request
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    const int64_t n = mb->n;
-    const int C = mb->C, nfeat = mb->nfeat;
-    const double* rows = mb->rows;
-    double* out = mb->out;
-    const int fast = mb->fast;
-    __syncthreads();  // every wave has read the command before the host may write the next
     if (fast)
       for (int64_t e = 0; e < n; ++e)
         small_epoch<true>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, guard, sh);
     else
       for (int64_t e = 0; e < n; ++e)
-        small_epoch<false>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, Guard{nullptr, nullptr, nullptr}, sh);
+        small_epoch<false>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat,
+                           Guard{nullptr, nullptr, nullptr}, sh);
     __threadfence_system();  // this thread's rows reach the host before the flag below
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    last = go;
+    if (tid == 0) __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = seq;
   }
 }
 

@@ -48,15 +48,20 @@ bool features_small_supported(int C);
 // The resident small-batch server (eegfx_ctx_set_mailbox): a host-mapped command block, written
 // by the host except `done` (the device's last completed request).
 struct MailboxCmd {
-  uint32_t req;   // request sequence number, incremented by the host after the fields below
-  uint32_t done;  // the last request whose rows are in `out` (device)
+  // The request word, written last by the host (release): sequence number << 32 | fast << 31 |
+  // (C - 1) << 26 | (nfeat - 1) << 21 | n -- the whole request in one aligned 64-bit load, so the
+  // kernel needs no second round trip across the host link for its fields.
+  uint64_t req;
+  uint32_t done;  // the last sequence number whose rows are in `out` (device)
   uint32_t stop;  // 1: the kernel returns
-  int32_t fast;   // numerics of the request (1 = EEGFX_FMA)
-  int64_t n;      // epochs
-  int32_t C, nfeat;
+  // staging, fixed while a server runs (growing it stops the server first); read at kernel start
   const double* rows;  // device-mapped pinned [n][C][512] window doubles
   double* out;         // device-mapped pinned [n][C * nfeat] rows
 };
+inline uint64_t mailbox_request(uint32_t seq, bool fast, int C, int nfeat, int64_t n) {
+  return (uint64_t)seq << 32 | (uint64_t)(fast ? 1 : 0) << 31 | (uint64_t)(C - 1) << 26 |
+         (uint64_t)(nfeat - 1) << 21 | (uint64_t)n;
+}
 hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
                                    const Guard& guard);
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,

@@ -376,21 +376,22 @@ struct C32Shared {
 };
 
 // Filter bank, normalisation and store of epoch e from its staged window (published by a
-// barrier); b = this lane's baseline.  Ends with every wave done reading `win` and sh.feat.
+// barrier); this lane's channel c = 8 w + lane / 8 has column col_c, resolution r and baseline b
+// (loaded by the caller, so no memory access of the common path follows a DMA it must not wait
+// for).  Ends with every wave done reading `win` and sh.feat.
 template <bool FAST, bool STREAM>
 __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int64_t n_frames,
                                             const ChanSel& sel, const float* __restrict__ base,
-                                            int64_t e, int64_t B, float b, uint8_t* win,
-                                            C32Shared& sh, double* __restrict__ out,
+                                            int64_t e, int64_t B, float b, int col_c, float r,
+                                            uint8_t* win, C32Shared& sh, double* __restrict__ out,
                                             const Guard& guard, int tid) {
   using K = C32;
   constexpr int C = K::C, FB = K::FB, SEGQ = K::SEGQ, F = K::F;
   const int lane = tid & 63, w = tid >> 6;
   const int c = w * 8 + (lane >> 3), s = lane & 7;
-  const uint8_t* eb = win + (int)(B & 15) + sel.col[c] * 2;
+  const uint8_t* eb = win + (int)(B & 15) + col_c * 2;
   const uint8_t* own = eb + 16 * SEGQ * s;
   const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
-  const float r = sel.res[c];
   double a6, d6;
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
@@ -500,10 +501,12 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   const int64_t e = (int64_t)xcd_tile(blockIdx.x, gridDim.x);
   const int64_t B = c32_window(pos, e, n_frames);
   (void)c32_issue<STREAM>(raw, n_frames * C32::FB, B, win, w, lane);
-  const float b = base[e * C32::C + w * 8 + (lane >> 3)];
+  const int c = w * 8 + (lane >> 3);
+  const float b = base[e * C32::C + c];
   dma_drain();
   __syncthreads();
-  c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, win, sh, out, guard, tid);
+  c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, sel.col[c], sel.res[c], win, sh,
+                            out, guard, tid);
 }
 
 // The same epochs with the next window in flight: a persistent grid (two workgroups per CU, two
@@ -522,14 +525,19 @@ __global__ __launch_bounds__(256) void window_c32_pp_kernel(
   const int64_t G = gridDim.x, g = blockIdx.x;
   const int64_t e_begin = g * n / G, e_end = (g + 1) * n / G;
   if (e_begin >= e_end) return;  // uniform per workgroup
+  const int c = w * 8 + (lane >> 3);
+  int col_c = sel.col[c];
+  float r = sel.res[c];
+  asm volatile("" : "+v"(col_c), "+v"(r));  // in registers before any DMA: no wait inside the loop
   int64_t B = c32_window(pos, e_begin, n_frames);
   bool full = c32_issue<STREAM>(raw, nbytes, B, win[0], w, lane);
   int64_t B_next = e_begin + 1 < e_end ? c32_window(pos, e_begin + 1, n_frames) : 0;
   for (int64_t e = e_begin; e < e_end; ++e) {
     const int cur = (int)((e - e_begin) & 1);
-    // loads of this epoch and of the window after next, before the next DMAs leave (vmcnt below
-    // then waits for nothing issued after them)
-    const float b = base[e * C32::C + w * 8 + (lane >> 3)];
+    // loads of this epoch and of the window after next complete before the next DMAs leave, so
+    // the vmcnt below (and the compiler's own waits) wait for nothing issued after them
+    float b = base[e * C32::C + c];
+    asm volatile("" : "+v"(b));
     const int64_t B_after = e + 2 < e_end ? c32_window(pos, e + 2, n_frames) : 0;
     bool full_next = true;
     const bool more = e + 1 < e_end;
@@ -538,7 +546,8 @@ __global__ __launch_bounds__(256) void window_c32_pp_kernel(
     else if (w == 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();  // epoch e's window is visible to every wave
-    c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, win[cur], sh, out, guard, tid);
+    c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, col_c, r, win[cur], sh, out,
+                              guard, tid);
     __syncthreads();  // every wave is done with win[cur] and sh before they are reused
     B = B_next;
     B_next = B_after;

@@ -91,6 +91,26 @@ def main():
                 "ceiling_ms": round(step, 4), "bytes_per_epoch": 4064,
                 "hbm_frac_at_ceiling": round(STEP_BYTES_C3 / (step * 1e-3) / HBM_PEAK, 4),
                 "measured_ms_sustained": round(bms + w["kernel_ms_sustained"], 4)}
+    if os.path.exists(f"{src}/step.txt") and os.path.exists(f"{src}/baseline.txt"):
+        # the per-step energy budget: at the 1.4 kW socket cap a step cannot take
+        # less than its energy / 1,400 W; the energies of the two passes from their own sustained
+        # runs (watts x launch time), against the step measured back to back
+        sw, smhz, _ = smi(f"{src}/step_smi.txt")
+        sms = probe_ms(f"{src}/step.txt")
+        bw, _, _ = smi(f"{src}/baseline_smi.txt")
+        bms = probe_ms(f"{src}/baseline.txt")
+        w = res["kernels"].get(KERNELS["c3"][0])
+        if w:
+            e_base = bw * bms * 1e-3
+            e_win = w["socket_W"] * w["kernel_ms_sustained"] * 1e-3
+            t_min = (e_base + e_win) / 1400.0 * 1e3
+            res["energy_budget_c3"] = {
+                "baseline_J": round(e_base, 4), "window_J_at_cap": round(e_win, 4),
+                "step_J_measured": round(sw * sms * 1e-3, 4), "step_W": sw,
+                "step_clock_MHz": round(smhz), "step_ms_sustained": sms,
+                "min_step_ms_at_1400W": round(t_min, 4),
+                "whole_path_frac_at_energy_bound": round(STEP_BYTES_C3 / (t_min * 1e-3) / HBM_PEAK, 4),
+                "step_ms_for_frac_0.60": round(STEP_BYTES_C3 / (0.6 * HBM_PEAK) * 1e3, 4)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1)[:3000])
 
