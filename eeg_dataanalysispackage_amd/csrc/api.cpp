@@ -153,18 +153,25 @@ struct eegfx_ctx {
   DevBuf raw, pos, out, scratch, fused;
   DevBuf lr_x, lr_y, lr_state, lr_part, lr_mask;  // logistic regression (eegfx_logreg_*)
   PinBuf pin_in, pin_out;                // small-batch extract_features staging (zero-copy)
-  // The fma numerics' conditioning guard (guard.h): device words (the flagged-row count of the
-  // current window_wide_kernel launch; at +8 B the running total of recomputed rows; at +16 B the
-  // running total of rows that went to the second stage) and the flagged-row list; guard_checked
-  // counts the rows that went through a guarded launch.
+  // The fma numerics' conditioning guard (guard.h): device memory holding the flagged-row count
+  // of the current window_wide_kernel launch (first 128 B), then the running totals of recomputed
+  // rows and of rows that went to the second stage, each spread over kGuardSlots lines; the
+  // flagged-row list; guard_checked counts the rows that went through a guarded launch.
+  static constexpr size_t kGuardDevBytes = 128 + 2 * kGuardSlotBytes;
   int* guard_dev = nullptr;
   DevBuf guard_list;
   int64_t guard_checked = 0;
+  unsigned long long* guard_recomputed_slots() const {
+    return (unsigned long long*)((char*)guard_dev + 128);
+  }
+  unsigned long long* guard_rechecked_slots() const {
+    return (unsigned long long*)((char*)guard_dev + 128 + kGuardSlotBytes);
+  }
   Guard guard_for(int64_t n) {
     if (numerics == EEGFX_EXACT) return Guard{nullptr, nullptr, nullptr};
     guard_checked += n;
     return Guard{guard_dev, (int64_t*)guard_list.get(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1)),
-                 (unsigned long long*)(guard_dev + 2), (unsigned long long*)(guard_dev + 4)};
+                 guard_recomputed_slots(), guard_rechecked_slots()};
   }
   void bind_buffers() {
     for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
@@ -224,8 +231,7 @@ struct eegfx_ctx {
     // the staging a server reads is fixed for its lifetime (growing it stops the server first)
     mb_host->rows = pin_in.p ? (const double*)pin_in.device_ptr() : nullptr;
     mb_host->out = pin_out.p ? (double*)pin_out.device_ptr() : nullptr;
-    const Guard g{guard_dev, nullptr, (unsigned long long*)(guard_dev + 2),
-                  (unsigned long long*)(guard_dev + 4)};
+    const Guard g{guard_dev, nullptr, guard_recomputed_slots(), guard_rechecked_slots()};
     HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks, g));
     mb_live = true;
   }
@@ -717,8 +723,8 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     HIP_CHECK(hipHostMalloc((void**)&c->err_host, sizeof(int), hipHostMallocMapped));
     *c->err_host = 0;
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
-    HIP_CHECK(hipMalloc((void**)&c->guard_dev, 24));
-    HIP_CHECK(hipMemset(c->guard_dev, 0, 24));
+    HIP_CHECK(hipMalloc((void**)&c->guard_dev, eegfx_ctx::kGuardDevBytes));
+    HIP_CHECK(hipMemset(c->guard_dev, 0, eegfx_ctx::kGuardDevBytes));
     *out = c.release();
   });
 }
@@ -795,15 +801,18 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
   return guarded([&] {
     if (!ctx || !rows_checked || !rows_recomputed) fail(EEGFX_EINVAL, "null argument");
     ctx->activate();
-    unsigned long long tot[2] = {0, 0};  // recomputed, rechecked
-    HIP_CHECK(hipMemcpyAsync(tot, ctx->guard_dev + 2, sizeof(tot), hipMemcpyDeviceToHost,
-                             ctx->stream));
+    std::vector<unsigned long long> slots(2 * kGuardSlots * kGuardSlotWords);
+    HIP_CHECK(hipMemcpyAsync(slots.data(), ctx->guard_recomputed_slots(), 2 * kGuardSlotBytes,
+                             hipMemcpyDeviceToHost, ctx->stream));
     ctx->drain();
+    unsigned long long tot[2] = {0, 0};  // recomputed, rechecked
+    for (int k = 0; k < 2; ++k)
+      for (int i = 0; i < kGuardSlots; ++i) tot[k] += slots[(size_t)(k * kGuardSlots + i) * kGuardSlotWords];
     *rows_checked = ctx->guard_checked;
     *rows_recomputed = (int64_t)tot[0];
     if (rows_rechecked) *rows_rechecked = (int64_t)tot[1];
     if (reset) {
-      HIP_CHECK(hipMemsetAsync(ctx->guard_dev + 2, 0, sizeof(tot), ctx->stream));
+      HIP_CHECK(hipMemsetAsync(ctx->guard_recomputed_slots(), 0, 2 * kGuardSlotBytes, ctx->stream));
       ctx->drain();
       ctx->guard_checked = 0;
     }

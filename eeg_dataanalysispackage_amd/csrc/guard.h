@@ -42,6 +42,13 @@ constexpr double kGuardK2Cascade = 1.62e-04;
 // the running total of rows recomputed under EXACT since the context was created, and of rows that
 // failed the a-priori test and went to the second stage (`rechecked`; may be null)
 // (eegfx_ctx_guard_stats / eegfx_ctx_guard_detail).  total == nullptr disables the guard (EXACT).
+// `total` and `rechecked` are running counters spread over kGuardSlots slots, one per 128-byte
+// line, a workgroup adding into slot blockIdx % kGuardSlots: one shared word took every
+// workgroup's atomic in turn, which at a 10 % flag rate cost as much as the kernel itself
+// (profiles/r05h: 0.733 -> 1.398 ms).  The host sums the slots.
+constexpr int kGuardSlots = 256;
+constexpr int kGuardSlotWords = 16;  // 128 B
+constexpr size_t kGuardSlotBytes = sizeof(unsigned long long) * kGuardSlots * kGuardSlotWords;
 struct Guard {
   int* count;
   int64_t* list;
@@ -68,8 +75,16 @@ __device__ __forceinline__ bool guard_fails(double acc, double k2, double sum_x2
   return !(acc >= k2 * sum_x2);
 }
 
+__device__ __forceinline__ void guard_slot_add(unsigned long long* slots, unsigned long long v) {
+  atomicAdd(slots + (blockIdx.x & (kGuardSlots - 1)) * kGuardSlotWords, v);
+}
+// rows recomputed with the EXACT cascade
+__device__ __forceinline__ void guard_count_recomputed(const Guard& g, unsigned long long rows) {
+  guard_slot_add(g.total, rows);
+}
+// rows that went to the second stage
 __device__ __forceinline__ void guard_count_rechecked(const Guard& g, int rows) {
-  if (g.rechecked && rows) atomicAdd(g.rechecked, (unsigned long long)rows);
+  if (g.rechecked && rows) guard_slot_add(g.rechecked, (unsigned long long)rows);
 }
 
 // Wave-wide minimum of packed int16 pairs (every lane gets it): the 16 lanes of a DPP row by

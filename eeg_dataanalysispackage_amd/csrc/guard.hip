@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kGuardBlock) void exact_rows_kernel(Src src, int nf
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, s = lane & 7;
   constexpr int SIG = kGuardBlock / 8;  // signals per pass
   const int cnt = *g.count;  // written by the guarded kernel before this launch
-  if (blockIdx.x == 0 && tid == 0 && cnt > 0) atomicAdd(g.total, (unsigned long long)cnt);
+  if (blockIdx.x == 0 && tid == 0 && cnt > 0) guard_count_recomputed(g, (unsigned long long)cnt);
   const int C = src.C;
   const int F = C * nfeat;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {  // uniform

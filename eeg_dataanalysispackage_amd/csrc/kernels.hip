@@ -244,7 +244,7 @@ __device__ __forceinline__ void staged_features(Smp smp, GSmp gsmp, const int* s
             C, 16, feat + F, feat, lane);
         if (lane == 0) {
           sh[0] = 1.0;  // the row is normalised
-          atomicAdd(guard.total, 1ull);
+          guard_count_recomputed(guard, 1ull);
         }
       }
       __syncthreads();
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
     uint64_t flagged = __ballot(fails);
     if (flagged) {
       wave_sync();
-      if (lane == 0) atomicAdd(guard.total, (unsigned long long)__popcll(flagged));
+      if (lane == 0) guard_count_recomputed(guard, (unsigned long long)__popcll(flagged));
       do {
         const int e = __ffsll((unsigned long long)flagged) - 1;
         const double* row = ep + (e0 + e) * C * (int64_t)row_stride + skip;
@@ -876,7 +876,7 @@ __device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows,
       const double acc = sum_squares();
       if (lane == 0) {
         sh.norm = sqrt(acc);
-        atomicAdd(guard.total, 1ull);
+        guard_count_recomputed(guard, 1ull);
       }
     }
     __syncthreads();

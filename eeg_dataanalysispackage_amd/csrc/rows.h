@@ -79,7 +79,7 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
       }
       if (lane == 0) {
         guard_count_rechecked(g, __popcll(flagged));
-        if (left) atomicAdd(g.total, (unsigned long long)__popcll(left));
+        if (left) guard_count_recomputed(g, (unsigned long long)__popcll(left));
       }
       for (; left; left &= left - 1) {
         const int e1 = __ffsll((unsigned long long)left) - 1;

@@ -463,7 +463,7 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
             C, 16, (double*)win, feat, lane);
         if (lane == 0) {
           sh.norm1 = 1.0;  // the row is normalised
-          atomicAdd(guard.total, 1ull);
+          guard_count_recomputed(guard, 1ull);
         }
       }
       __syncthreads();

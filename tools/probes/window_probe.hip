@@ -53,14 +53,17 @@ int main() {
   (void)hipMemcpy(pos, hp.data(), n * 8, hipMemcpyHostToDevice);
   eegfx::ChanSel sel{};
   for (int c = 0; c < ct; ++c) { sel.col[c] = c; sel.res[c] = 0.1f; }
-  // the product's fma guard state (eegfx_ctx: count, running total, list)
+  // the product's fma guard state (eegfx_ctx: count, the two slot-spread running totals, list)
   int* gdev;
   int64_t* glist;
-  (void)hipMalloc(&gdev, 16);
-  (void)hipMemset(gdev, 0, 16);
+  const size_t gbytes = 128 + 2 * eegfx::kGuardSlotBytes;
+  (void)hipMalloc(&gdev, gbytes);
+  (void)hipMemset(gdev, 0, gbytes);
   (void)hipMalloc(&glist, n * 8);
-  const eegfx::Guard g = fast ? eegfx::Guard{gdev, glist, (unsigned long long*)(gdev + 2)}
-                              : eegfx::Guard{nullptr, nullptr, nullptr};
+  const eegfx::Guard g =
+      fast ? eegfx::Guard{gdev, glist, (unsigned long long*)((char*)gdev + 128),
+                          (unsigned long long*)((char*)gdev + 128 + eegfx::kGuardSlotBytes)}
+           : eegfx::Guard{nullptr, nullptr, nullptr};
   auto baseline = [&] {
     if (wide) (void)eegfx::launch_baseline_any(0, raw, 0, nf, ct, sel, ct, pos, n, base, nullptr, g.count);
     else (void)eegfx::launch_fused_baseline(0, raw, nf, ct, sel, ct, pos, n, base, nullptr, nullptr);
