@@ -150,11 +150,11 @@ def traffic_from_profiles(workload_key):
     return best
 
 
-CEILING_FILE = os.path.join("profiles", "r04_ceiling.json")
+CEILING_FILE = os.path.join("profiles", "r05_ceiling.json")
 
 
 def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
-    """The attainable bound of the dominant kernel (profiles/r04_ceiling.json, written by
+    """The attainable bound of the dominant kernel (profiles/r05_ceiling.json, written by
     tools/ceiling_summary.py): its VALU issue time at the clock the chip holds under the kernel's
     own sustained power draw (SQ counters + amd-smi under load), scaled to this launch's epochs,
     next to the live kernel time."""
@@ -178,8 +178,10 @@ def ceiling_from_profiles(C, numerics, n, kernel_ms, kernel_bytes):
 def whole_path_ceiling(C, numerics, n, step_ms, bpe):
     """The attainable bound of the whole step: the baseline pass at its own measured time (it
     runs below the power cap, bound by its memory pattern) plus the window kernel's VALU bound,
-    scaled to this launch's epochs (profiles/r04_ceiling.json): the c3 step (baseline_kernel +
-    window_kernel) and the configs[3] step (baseline_any_kernel + window_c32_kernel)."""
+    scaled to this launch's epochs (profiles/r05_ceiling.json): the c3 step (baseline_kernel +
+    window_kernel) and the configs[3] step (baseline_any_kernel + window_c32_kernel).  For c3 also
+    the energy bound: the step's measured energy (baseline pass below the cap + window kernel at
+    the cap) over the 1.4 kW cap, the shortest step this instruction stream allows."""
     if numerics != "fma" or C not in (3, 32):
         return None
     try:
@@ -195,9 +197,17 @@ def whole_path_ceiling(C, numerics, n, step_ms, bpe):
     except Exception:
         return None
     ms = b + w["ceiling_ms"] * n / w["epochs_per_launch"]
-    return {"ms": round(ms, 4), "frac": round(n * bpe / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "step_over_ceiling": round(ms / step_ms, 4),
-            "baseline_kernel_ms_alone": b, "source": CEILING_FILE}
+    out = {"ms": round(ms, 4), "frac": round(n * bpe / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "step_over_ceiling": round(ms / step_ms, 4),
+           "baseline_kernel_ms_alone": b, "source": CEILING_FILE}
+    e = d.get("energy_budget_c3") if C == 3 else None
+    if e:
+        ems = e["min_step_ms_at_1400W"] * n / w["epochs_per_launch"]
+        out["energy_bound"] = {"ms": round(ems, 4),
+                               "frac": round(n * bpe / (ems * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                               "step_over_bound": round(ems / step_ms, 4),
+                               "step_J": e["step_J_measured"], "cap_W": e["step_W"]}
+    return out
 
 
 _JSON_OUT = None

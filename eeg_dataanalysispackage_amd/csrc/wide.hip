@@ -25,12 +25,6 @@
 #include "launch.h"
 #include "lds_dma.h"
 
-// configs[3]'s 32-channel kernel as a persistent grid with the next window in flight
-// (window_c32_pp_kernel); 0 = one epoch per workgroup (window_c32_kernel)
-#ifndef EEGFX_C32_PP
-#define EEGFX_C32_PP 0
-#endif
-
 namespace eegfx {
 namespace dev {
 
@@ -509,52 +503,6 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
                             out, guard, tid);
 }
 
-// The same epochs with the next window in flight: a persistent grid (two workgroups per CU, two
-// window buffers each, 70 KB) walks a contiguous range of epochs per workgroup; epoch e+1's window
-// DMA leaves before epoch e's filter bank starts, and only e's DMAs are waited for (vmcnt = the
-// rows in flight).  A window that crosses either end of the recording drains everything.
-template <bool FAST, bool STREAM>
-__global__ __launch_bounds__(256) void window_c32_pp_kernel(
-    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
-    const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
-    double* __restrict__ out, Guard guard) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[2][C32::EQ * 16];
-  __shared__ C32Shared sh;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t nbytes = n_frames * C32::FB;
-  const int64_t G = gridDim.x, g = blockIdx.x;
-  const int64_t e_begin = g * n / G, e_end = (g + 1) * n / G;
-  if (e_begin >= e_end) return;  // uniform per workgroup
-  const int c = w * 8 + (lane >> 3);
-  int col_c = sel.col[c];
-  float r = sel.res[c];
-  asm volatile("" : "+v"(col_c), "+v"(r));  // in registers before any DMA: no wait inside the loop
-  int64_t B = c32_window(pos, e_begin, n_frames);
-  bool full = c32_issue<STREAM>(raw, nbytes, B, win[0], w, lane);
-  int64_t B_next = e_begin + 1 < e_end ? c32_window(pos, e_begin + 1, n_frames) : 0;
-  for (int64_t e = e_begin; e < e_end; ++e) {
-    const int cur = (int)((e - e_begin) & 1);
-    // loads of this epoch and of the window after next complete before the next DMAs leave, so
-    // the vmcnt below (and the compiler's own waits) wait for nothing issued after them
-    float b = base[e * C32::C + c];
-    asm volatile("" : "+v"(b));
-    const int64_t B_after = e + 2 < e_end ? c32_window(pos, e + 2, n_frames) : 0;
-    bool full_next = true;
-    const bool more = e + 1 < e_end;
-    if (more) full_next = c32_issue<STREAM>(raw, nbytes, B_next, win[cur ^ 1], w, lane);
-    if (!more || !full || !full_next) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (w == 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    __syncthreads();  // epoch e's window is visible to every wave
-    c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, col_c, r, win[cur], sh, out,
-                              guard, tid);
-    __syncthreads();  // every wave is done with win[cur] and sh before they are reused
-    B = B_next;
-    B_next = B_after;
-    full = full_next;
-  }
-}
-
 }  // namespace dev
 
 namespace {
@@ -653,17 +601,10 @@ static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, in
              : launch_wide_t<T, FA, 1>(st, raw, n_frames, ct, sel, C, pos, base, n, out, guard);
   if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) {  // configs[3]
     const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
-#if EEGFX_C32_PP
-    const dim3 g((unsigned)std::min<int64_t>(n, 2 * 256));  // two resident workgroups per CU
-#define EEGFX_C32(FA, NTV) \
-    hipLaunchKernelGGL((dev::window_c32_pp_kernel<FA, NTV>), g, dim3(256), 0, st, \
-                       (const uint8_t*)raw, n_frames, sel, pos, base, n, out, guard)
-#else
     const dim3 g((unsigned)n);
 #define EEGFX_C32(FA, NTV) \
     hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV>), g, dim3(256), 0, st, (const uint8_t*)raw, \
                        n_frames, sel, pos, base, n, out, guard)
-#endif
     if (fast) { if (nt) EEGFX_C32(true, true); else EEGFX_C32(true, false); }
     else { if (nt) EEGFX_C32(false, true); else EEGFX_C32(false, false); }
 #undef EEGFX_C32
