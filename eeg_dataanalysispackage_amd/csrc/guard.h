@@ -10,7 +10,9 @@
 //     |f_fma|^2 >= K2 * sum_c X_c^2,     K2 = (2 / 0.5e-9)^2 * 8 (E_a6^2 + E_d6^2) * 1.25.
 // A row that fails the test -- its features are close to rounding noise, or X_c is loose -- goes
 // to a second stage: the wave that normalises it measures the row's own max |x| per channel
-// (guard_measured_x2_wave) and tests again with that X.  Only rows that still fail (e.g. a window
+// (guard_measured_x2_wave) and tests again with that X -- in the 3-channel kernels the cheaper
+// 3 max_c X_c^2 >= sum_c X_c^2 (rows.h recheck_c3: one wave reduction instead of three; the pass
+// is VALU-bound at the power cap).  Only rows that still fail (e.g. a window
 // in the filters' null space, an alternating +-A signal) are recomputed with the EXACT filter bank,
 // value-identical to the reference, by the same wave inside the same kernel
 // (dwt8_exact_row_wave): the 3-channel window kernel, the 32-channel kernel, the one-pass kernels,
@@ -95,12 +97,30 @@ __device__ __forceinline__ uint32_t wave_pk_min_i16(uint32_t v) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(s2, a),
                                                                   __builtin_bit_cast(s2, b)));
   };
-  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
-  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
-  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
-  v = mn(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
   v = mn(v, (uint32_t)__shfl_xor((int)v, 16, 64));
   return mn(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+}
+
+// lane j's v (j wave-uniform), as a wave-uniform value
+__device__ __forceinline__ double lane_value(double v, int j) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
+// Wave-wide maximum of unsigned words (every lane gets it), the same moves as wave_pk_min_i16.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__shfl_xor((int)v, 16, 64));
+  return max(v, (uint32_t)__shfl_xor((int)v, 32, 64));
 }
 
 // Packs a lane's (min, max) of int16 samples as (min, ~max) so that one packed minimum reduces
@@ -139,10 +159,10 @@ __device__ __forceinline__ double guard_measured_x2_wave(Sample sample, Decode d
       hi = max(hi, v);
     }
     uint32_t p = guard_pack_minmax(lo, hi);  // reduced over the DPP row = this channel's lanes
-    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0xB1, 0xF, 0xF, false));
-    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x4E, 0xF, 0xF, false));
-    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x141, 0xF, 0xF, false));
-    p = mn(p, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x140, 0xF, 0xF, false));
+    p = mn(p, (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0xB1, 0xF, 0xF, true));
+    p = mn(p, (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0x4E, 0xF, 0xF, true));
+    p = mn(p, (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0x141, 0xF, 0xF, true));
+    p = mn(p, (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0x140, 0xF, 0xF, true));
     const double X = fmax(fabs(decode(c, (float)guard_unpack_min(p))),
                           fabs(decode(c, (float)guard_unpack_max(p))));
     double x2 = c0 + grp < C ? X * X : 0.0;

@@ -785,14 +785,6 @@ struct SmallLds {
   int redo;
 };
 
-// lane j's v (j wave-uniform), as a wave-uniform value
-__device__ __forceinline__ double lane_value(double v, int j) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
-  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-}
-
 // One epoch (its C x 512 window doubles at `src`, 16-byte aligned) -> its row at `dst`, by a
 // workgroup of 256 threads (uniform control flow; ends with a barrier).
 template <bool FAST>

@@ -74,7 +74,7 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
       uint64_t left = 0;                  // rows that fail the measured test too
       for (uint64_t f = flagged; f; f &= f - 1) {
         const int e1 = __ffsll((unsigned long long)f) - 1;
-        const double acc_e = __shfl(acc, e1, 64);
+        const double acc_e = lane_value(acc, e1);  // e1 is wave-uniform
         if (guard_fails(acc_e, kGuardK2Collapsed, recheck(e1 >> 3))) left |= 1ull << e1;
       }
       if (lane == 0) {
@@ -114,10 +114,12 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
 // wave: lane l reads frames 64 (l >> 3) + 8 (l & 7) .. + 7 of the window, all three channels --
 // from the staged window `lds` (the window kernel's layout: segment s at 16 SEGQ s bytes past the
 // epoch's misalignment) or, when from_raw, from the recording (zero past its end, the reference's
-// padding) -- keeps each channel's min and max raw sample, reduces them over the wave as packed
-// int16 pairs (DPP, no LDS round trips), and returns sum_c X_c^2 with X_c = max(|x(min)|,
-// |x(max)|): x = fl(fl(raw * r) - b) is monotone in raw.  One LDS (or memory) round trip for all
-// 24 samples of a lane.
+// padding) -- keeps each channel's min and max raw sample, decodes those six extremes exactly as
+// the kernel decodes every sample (x = fl(fl(raw * r) - b) is monotone in raw, so they bound the
+// lane's |x|), and takes one wave maximum: X = max_c max |x_c|.  It returns 3 X^2 >= sum_c X_c^2,
+// a rigorous bound at most 3x looser than the per-channel sum (which would cost three wave
+// reductions: this pass is VALU-bound at the power cap, ~50 instead of ~100 VALU per row).
+// One LDS (or memory) round trip for all 24 samples of a lane.
 template <int FB, int SEGQ>
 __device__ __forceinline__ double recheck_c3(const uint8_t* __restrict__ raw, int64_t n_frames,
                                              const ChanSel& sel, int64_t W,
@@ -128,13 +130,21 @@ __device__ __forceinline__ double recheck_c3(const uint8_t* __restrict__ raw, in
   if (from_raw) {  // wave-uniform
     const int64_t B = W & ~(int64_t)1;
     const int64_t g0 = B / FB + f0;
+    if (B / FB + kWin <= n_frames) {  // wave-uniform: the whole window inside, no per-load test
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        v[c][i] = g0 + i < n_frames
-                      ? *(const int16_t*)(raw + B + (int64_t)(f0 + i) * FB + 2 * sel.col[c])
-                      : 0;
+        for (int c = 0; c < 3; ++c)
+          v[c][i] = *(const int16_t*)(raw + B + (int64_t)(f0 + i) * FB + 2 * sel.col[c]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          v[c][i] = g0 + i < n_frames
+                        ? *(const int16_t*)(raw + B + (int64_t)(f0 + i) * FB + 2 * sel.col[c])
+                        : 0;
+    }
   } else {
     const uint8_t* p = lds + ((uint32_t)W & 14u) + 16 * SEGQ * (lane >> 3) +
                        FB * 8 * (lane & 7);
@@ -143,7 +153,8 @@ __device__ __forceinline__ double recheck_c3(const uint8_t* __restrict__ raw, in
 #pragma unroll
       for (int c = 0; c < 3; ++c) v[c][i] = *(const int16_t*)(p + FB * i + 2 * sel.col[c]);
   }
-  double sx = 0.0;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  float xm = 0.0f;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     int mn = v[c][0], mx = v[c][0];
@@ -152,15 +163,16 @@ __device__ __forceinline__ double recheck_c3(const uint8_t* __restrict__ raw, in
       mn = min(mn, v[c][i]);
       mx = max(mx, v[c][i]);
     }
-    const uint32_t pr = wave_pk_min_i16(guard_pack_minmax(mn, mx));
+    // (lo, hi) decoded as one pair: packed fp32 multiply and add, each lane rounded as the
+    // scalar fl(fl(raw * r) - b)
     const float r = sel.res[c], bc = b[c];
-    float lo = (float)guard_unpack_min(pr) * r, hi = (float)guard_unpack_max(pr) * r;
-    lo = lo - bc;
-    hi = hi - bc;
-    const double X = fmax(fabs((double)lo), fabs((double)hi));
-    sx += X * X;
+    f32x2 x = f32x2{(float)mn, (float)mx} * f32x2{r, r};
+    x = x + f32x2{-bc, -bc};
+    xm = fmaxf(xm, fmaxf(fabsf(x.x), fabsf(x.y)));
   }
-  return sx * (1.0 + 0x1p-20);
+  // |x| >= 0: its bit pattern orders like the value
+  const double X = (double)__uint_as_float(wave_max_u32(__float_as_uint(xm)));
+  return (X * X) * (3.0 * (1.0 + 0x1p-20));  // the constant is exact: 3 + 3 * 2^-20
 }
 
 }  // namespace dev

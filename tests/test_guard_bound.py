@@ -101,9 +101,10 @@ def test_exact_cascade_within_derived_bound(kind):
         assert abs(Fraction(float(f[i])) - f_exact[i]) <= Fraction(E * X), (kind, i)
 
 
-def crude_ratio(raw, pos, measured=False):
+def crude_ratio(raw, pos, measured=False, three_max=False):
     """|f| / sqrt(sum_c X_c^2) per epoch with the a-priori int16 bound of guard.h, or (measured)
-    with the second stage's X_c = max |x_c| over the window (guard_measured_x2_wave)."""
+    with the second stage's X_c = max |x_c| over the window (guard_measured_x2_wave), or
+    (three_max) with the 3-channel kernels' cheaper 3 max_c X_c^2 >= sum_c X_c^2 (recheck_c3)."""
     ep = oracle.decode_epochs(raw, [0, 1, 2], [0.1] * 3, pos)
     feats = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
     out = []
@@ -122,6 +123,8 @@ def crude_ratio(raw, pos, measured=False):
             else:
                 X = (32768 * abs(float(np.float32(0.1))) + abs(float(b))) * (1 + 2.0 ** -20)
             sx += X * X
+        if three_max:
+            sx = 3 * max(float(np.max(np.abs(ep[e, c, 175:687]))) for c in range(3)) ** 2 * (1 + 2.0 ** -20)
         out.append(nf / np.sqrt(sx))
     return np.array(out)
 
@@ -156,7 +159,11 @@ def test_flat_windows_certified_by_the_second_stage():
     meas = crude_ratio(raw, allpos, measured=True)
     assert np.sum(crude * crude < k2) >= 9          # the a-priori test flags the flat windows
     assert np.all(meas * meas >= k2), meas.min()     # the measured one certifies all of them
+    three = crude_ratio(raw, allpos, three_max=True)  # and so does recheck_c3's looser form,
+    assert np.all(three * three >= 1e5 * k2), three.min()  # with five orders of magnitude to spare
     t = np.arange(12000)[:, None]
     alt = (np.where(t % 2 == 0, 1, -1) * 700 - 2000 + np.zeros((1, 3))).astype(np.int16)
     r = crude_ratio(alt, [1000, 2001, 3000], measured=True)
+    assert np.all(r * r < k2)
+    r = crude_ratio(alt, [1000, 2001, 3000], three_max=True)
     assert np.all(r * r < k2)
