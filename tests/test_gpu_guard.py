@@ -271,6 +271,28 @@ def test_flat_windows_certified_by_second_stage_every_int16_kernel(ctx):
         assert redone == 0 and rechecked >= len(flat), (ct, rechecked, redone)
 
 
+def test_flat_window_past_the_recording_end_rechecked_from_the_recording(ctx):
+    """A silent stretch (raw 0, so x = 0 after the baseline) running into the end of the recording:
+    the last marker's window is zero-padded past the end (copyOfRange) and is the first epoch of
+    its sub-tile, so its second stage reads the recording with the per-frame end test (the window
+    kernel's rows lie over that epoch's staged window).  Certified, not recomputed; the row equals
+    the oracle (0/0 -> NaN)."""
+    n = 9
+    raw, pos, _ = flat_recording(n, 1000, 3, n + 1)
+    raw = raw[:pos[8] + 400].copy()
+    raw[pos[8] - 100:] = 0
+    want = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
+    for name, run in (("fused", lambda: ctx.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, pos)),
+                      ("one_pass", lambda: ctx.process_recording_epochs(raw, 3, [0, 1, 2],
+                                                                        [0.1] * 3, pos)[0])):
+        ctx.guard_detail(reset=True)
+        got = run()
+        checked, rechecked, redone = ctx.guard_detail()
+        assert np.isnan(want[8]).all() and np.isnan(got[8]).all(), name
+        assert within(got[:8], want[:8]), name
+        assert rechecked >= 1 and redone == 0, (name, rechecked, redone)
+
+
 def test_flat_and_null_windows_mixed(ctx):
     """Flat windows (certified by the second stage) and null-space windows (recomputed) in one
     sub-tile: the counters separate them and the null rows equal the oracle value for value."""
