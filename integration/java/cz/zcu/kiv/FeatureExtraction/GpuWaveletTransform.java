@@ -14,6 +14,10 @@ public class GpuWaveletTransform implements IFeatureExtraction {
     private static final int CHANNELS = 3;
     private static final int POSTSTIMULUS = 750;   // Const.POSTSTIMULUS_VALUES
 
+    /** -Deegfx.mailbox=true: every thread's context keeps a resident workgroup serving its
+     *  one-epoch calls without a kernel launch each (eegfx_ctx_set_mailbox; DESIGN.md section 9). */
+    private static final boolean MAILBOX = Boolean.getBoolean("eegfx.mailbox");
+
     // One device context per calling thread: extractFeatures is reached concurrently from the
     // Spark local[*] executor threads (LogisticRegressionClassifier.java:50,90), and an eegfx
     // context drives one stream.
@@ -21,6 +25,8 @@ public class GpuWaveletTransform implements IFeatureExtraction {
         @Override protected Long initialValue() {
             long c = nativeCreate(0);
             if (c == 0) throw new IllegalStateException(nativeLastError());
+            if (MAILBOX && nativeSetMailbox(c, true) != 0)
+                throw new IllegalStateException(nativeLastError());
             return c;
         }
     };
@@ -83,6 +89,7 @@ public class GpuWaveletTransform implements IFeatureExtraction {
     }
 
     private static native long nativeCreate(int device);
+    private static native int nativeSetMailbox(long ctx, boolean on);
     private static native int nativeExtract(long ctx, double[] epochs, int n, int C, int name,
                                             int epochSize, int skip, int featureSize, double[] out);
     private static native String nativeLastError();

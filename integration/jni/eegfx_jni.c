@@ -23,6 +23,13 @@ Java_cz_zcu_kiv_FeatureExtraction_GpuWaveletTransform_nativeCreate(JNIEnv* env, 
 }
 
 JNIEXPORT jint JNICALL
+Java_cz_zcu_kiv_FeatureExtraction_GpuWaveletTransform_nativeSetMailbox(JNIEnv* env, jclass k,
+                                                                      jlong ctx, jboolean on) {
+  (void)env; (void)k;
+  return eegfx_shim_ctx_set_mailbox(ctx, on ? 1 : 0);
+}
+
+JNIEXPORT jint JNICALL
 Java_cz_zcu_kiv_FeatureExtraction_GpuWaveletTransform_nativeExtract(
     JNIEnv* env, jclass k, jlong ctx, jdoubleArray epochs, jint n, jint C, jint name,
     jint epochSize, jint skip, jint featureSize, jdoubleArray out) {

@@ -25,6 +25,10 @@ int eegfx_shim_ctx_destroy(int64_t ctx) {
   return eegfx_ctx_destroy((eegfx_ctx*)(intptr_t)ctx);
 }
 
+int eegfx_shim_ctx_set_mailbox(int64_t ctx, int32_t enable) {
+  return eegfx_ctx_set_mailbox((eegfx_ctx*)(intptr_t)ctx, enable ? 1 : 0);
+}
+
 int eegfx_shim_extract(int64_t ctx, const double* epochs, int32_t n, int32_t C, int32_t name,
                        int32_t epoch_size, int32_t skip, int32_t feature_size, double* out) {
   return eegfx_extract_features_f64((eegfx_ctx*)(intptr_t)ctx, epochs, n, C, name, epoch_size,

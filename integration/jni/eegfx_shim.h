@@ -33,6 +33,9 @@ const char* eegfx_shim_exception_class(int status);
  * 0 on failure (eegfx_last_error has the text). */
 int64_t eegfx_shim_ctx_create(int32_t device);
 int eegfx_shim_ctx_destroy(int64_t ctx);
+/* opt-in resident per-epoch server of the context (eegfx_ctx_set_mailbox); GpuWaveletTransform
+ * turns it on for every executor thread's context when -Deegfx.mailbox=true */
+int eegfx_shim_ctx_set_mailbox(int64_t ctx, int32_t enable);
 /* nativeExtract: n epochs double[n][C][750] (flattened by the Java side from its double[][][]) ->
  * rows double[n][C * feature_size] in host memory (EEGFX_MEM_HOST: one epoch takes the
  * per-epoch latency kernel, batches the chunked-copy path). */

@@ -36,12 +36,16 @@ typedef struct {
   int64_t n;
   const double* epochs;
   double* rows;
+  int mailbox; /* -Deegfx.mailbox=true */
 } worker;
 
 static void* extract_per_epoch(void* arg) {  /* one executor thread, its own context */
   worker* w = (worker*)arg;
   const int64_t ctx = eegfx_shim_ctx_create(0);
   CHECK(ctx != 0, "thread %d ctx: %s", w->t, eegfx_last_error());
+  if (w->mailbox)
+    CHECK(eegfx_shim_ctx_set_mailbox(ctx, 1) == EEGFX_OK, "thread %d mailbox: %s", w->t,
+          eegfx_last_error());
   for (int64_t i = w->t; i < w->n; i += THREADS)
     CHECK(eegfx_shim_extract(ctx, w->epochs + i * C * POST, 1, C, 8, 512, 175, 16,
                              w->rows + i * F) == EEGFX_OK,
@@ -118,17 +122,21 @@ int main(int argc, char** argv) {
     }
   CHECK(esum == -253772.18676757812, "epoch sum %.17g (golden -253772.18676757812)", esum);
 
-  /* GpuWaveletTransform.extractFeatures, one epoch per call from THREADS threads */
+  /* GpuWaveletTransform.extractFeatures, one epoch per call from THREADS threads: launched per
+   * call, then with -Deegfx.mailbox=true (each thread's context serves from a resident workgroup) */
   double* rows = (double*)malloc(sizeof(double) * (size_t)n * F);
-  pthread_t th[THREADS];
-  worker w[THREADS];
-  for (int t = 0; t < THREADS; ++t) {
-    w[t] = (worker){t, n, epochs, rows};
-    CHECK(pthread_create(&th[t], NULL, extract_per_epoch, &w[t]) == 0, "pthread_create");
+  for (int mailbox = 0; mailbox < 2; ++mailbox) {
+    pthread_t th[THREADS];
+    worker w[THREADS];
+    memset(rows, 0, sizeof(double) * (size_t)n * F);
+    for (int t = 0; t < THREADS; ++t) {
+      w[t] = (worker){t, n, epochs, rows, mailbox};
+      CHECK(pthread_create(&th[t], NULL, extract_per_epoch, &w[t]) == 0, "pthread_create");
+    }
+    for (int t = 0; t < THREADS; ++t) pthread_join(th[t], NULL);
+    CHECK(memcmp(rows, feat, sizeof(double) * (size_t)n * F) == 0,
+          "per-epoch extractFeatures rows (mailbox %d) differ from getFeatures", mailbox);
   }
-  for (int t = 0; t < THREADS; ++t) pthread_join(th[t], NULL);
-  CHECK(memcmp(rows, feat, sizeof(double) * (size_t)n * F) == 0,
-        "per-epoch extractFeatures rows differ from getFeatures");
   /* extractFeaturesBatch */
   CHECK(eegfx_shim_extract(ctx, epochs, (int32_t)n, C, 8, 512, 175, 16, rows) == EEGFX_OK,
         "extractFeaturesBatch: %s", eegfx_last_error());
