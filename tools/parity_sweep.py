@@ -11,7 +11,11 @@ legal edges (pos = 100, windows past the end, pos - 100 = n_frames), then
   * every fifth case, eegfx_process_recording_streamed with a random chunk size (EXACT).
 EXACT must equal the oracle value for value (epochs always); fma within 1e-9 per feature.
 
-  python tools/parity_sweep.py [--cases 2000] [--seed0 0] [--out summary.json]
+`--flat` overwrites the spans [pos-100, pos+750) of about a third of each case's markers with
+held samples (flat, the value at pos-100) or zeros (silent): the rows the fma guard's first
+stage flags and its second stage certifies (the guard counters are added to the summary).
+
+  python tools/parity_sweep.py [--cases 2000] [--seed0 0] [--flat] [--out summary.json]
 """
 import argparse
 import json
@@ -25,7 +29,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def case(seed):
+def case(seed, flat=False):
     rng = np.random.default_rng(50_000 + seed)
     ct = int(rng.choice([1, 2, 3, 3, 3, 4, 5, 7, 8, 16, 32, 32, 40, 63, 64]))
     C = int(rng.integers(1, ct + 1)) if seed % 4 else ct
@@ -45,6 +49,13 @@ def case(seed):
         pos[-1] = nf + 100
     nfeat = int(rng.integers(1, 17))
     skip = int(rng.integers(0, 750 - 512 + 1))
+    if flat:  # a separate stream, so the unplanted cases stay those of earlier sweeps
+        prng = np.random.default_rng(90_000 + seed)
+        raw = raw.copy()
+        for p in pos[prng.random(n) < 0.35]:
+            lo, hi = max(0, int(p) - 100), min(nf, int(p) + 750)
+            if lo < hi:
+                raw[lo:hi] = raw[lo] if prng.integers(0, 2) else 0
     return raw, ct, cols, res, pos, nfeat, skip
 
 
@@ -52,12 +63,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=2000)
     ap.add_argument("--seed0", type=int, default=0)
+    ap.add_argument("--flat", action="store_true")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import torch
     import eeg_dataanalysispackage_amd as fx
     from oracle import oracle
     ex, fm = fx.Context(0, numerics="exact"), fx.Context(0, numerics="fma")
+    fm.guard_detail(reset=True)
     stats = {"cases": 0, "epochs": 0, "checks": 0, "mismatches": [], "max_fma_err": 0.0,
              "by_channels": {}}
     t0 = time.time()
@@ -71,7 +84,7 @@ def main():
         return err <= 1e-9, err
 
     for seed in range(a.seed0, a.seed0 + a.cases):
-        raw, ct, cols, res, pos, nfeat, skip = case(seed)
+        raw, ct, cols, res, pos, nfeat, skip = case(seed, a.flat)
         want = oracle.process_recording(raw, cols, res, pos)
         want_ep = oracle.decode_epochs(raw, cols, res, pos)
         want_x = oracle.extract_features(want_ep, nfeat=nfeat, skip=skip)
@@ -121,6 +134,9 @@ def main():
             last = time.time()
             print(f"{stats['cases']} cases, {len(stats['mismatches'])} mismatches, "
                   f"{last - t0:.0f} s", flush=True)
+    checked, rechecked, recomputed = fm.guard_detail()
+    stats["guard"] = {"rows_checked": checked, "rows_rechecked": rechecked,
+                      "rows_recomputed": recomputed, "flat": a.flat}
     ex.close()
     fm.close()
     stats["seconds"] = round(time.time() - t0, 1)
