@@ -284,10 +284,9 @@ struct eegfx_ctx {
     mb_last = std::chrono::steady_clock::now();
   }
   void release_mailbox() {
-    if (!mb_host) return;
-    mb_stop();
-    (void)hipStreamDestroy(mb_stream);
-    (void)hipHostFree(mb_host);
+    if (mb_host) mb_stop();
+    if (mb_stream) (void)hipStreamDestroy(mb_stream);
+    if (mb_host) (void)hipHostFree(mb_host);
     mb_host = nullptr;
     mb_dev = nullptr;
     mb_stream = nullptr;
@@ -776,15 +775,20 @@ int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable) {
       return;
     }
     if (ctx->mailbox) return;
-    HIP_CHECK(hipStreamCreateWithFlags(&ctx->mb_stream, hipStreamNonBlocking));
-    HIP_CHECK(hipHostMalloc((void**)&ctx->mb_host, sizeof(MailboxCmd),
-                            hipHostMallocMapped | hipHostMallocCoherent));
-    memset(ctx->mb_host, 0, sizeof(MailboxCmd));
-    HIP_CHECK(hipHostGetDevicePointer((void**)&ctx->mb_dev, ctx->mb_host, 0));
-    ctx->mb_seq = 0;
-    ctx->mb_launch();
-    ctx->mb_last = std::chrono::steady_clock::now();
-    ctx->mailbox = true;
+    ctx->mailbox = true;  // from here on release_mailbox undoes whatever was set up
+    try {
+      HIP_CHECK(hipStreamCreateWithFlags(&ctx->mb_stream, hipStreamNonBlocking));
+      HIP_CHECK(hipHostMalloc((void**)&ctx->mb_host, sizeof(MailboxCmd),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+      memset(ctx->mb_host, 0, sizeof(MailboxCmd));
+      HIP_CHECK(hipHostGetDevicePointer((void**)&ctx->mb_dev, ctx->mb_host, 0));
+      ctx->mb_seq = 0;
+      ctx->mb_launch();
+      ctx->mb_last = std::chrono::steady_clock::now();
+    } catch (...) {
+      ctx->release_mailbox();
+      throw;
+    }
   });
 }
 
