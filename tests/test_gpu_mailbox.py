@@ -92,3 +92,33 @@ def test_mailbox_concurrent_contexts_and_destroy(epochs):
         x.join(timeout=90)
     assert not any(x.is_alive() for x in th)
     assert errors == []
+
+
+@pytest.mark.parametrize("C,nfeat", [(1, 16), (5, 7), (16, 16)])
+def test_per_epoch_kernel_any_channel_count(C, nfeat):
+    """The per-epoch kernel beyond the 3-channel montage, launched and served resident: up to 16
+    channels (rows of up to 256 features, so the lane-ordered sum of squares takes four passes of
+    64) and feature sizes below 16, value-identical to the oracle under EXACT and within 1e-9
+    under fma."""
+    rng = np.random.default_rng(100 + C)
+    nf = 6000
+    raw = np.clip(rng.integers(-26000, -24000, size=(1, C)) +
+                  np.cumsum(rng.integers(-40, 41, size=(nf, C)), axis=0), -32768, 32767)
+    raw = raw.astype(np.int16)
+    ep = oracle.decode_epochs(raw, list(range(C)), [0.1] * C, [500, 1800, 3100, 4400])
+    want = oracle.extract_features(ep, nfeat=nfeat)
+    for numerics in ("exact", "fma"):
+        c = fx.Context(0, numerics=numerics)
+        try:
+            for mailbox in (False, True):
+                c.set_mailbox(mailbox)
+                got = np.concatenate([c.extract_features(ep[i:i + 1], feature_size=nfeat)
+                                      for i in range(len(ep))])
+                if numerics == "exact":
+                    assert eq(got, want), (C, nfeat, mailbox)
+                else:
+                    assert np.max(np.abs(got - want)) <= 1e-9, (C, nfeat, mailbox)
+                assert eq(c.extract_features(ep, feature_size=nfeat), got)  # the 4-epoch batch
+        finally:
+            c.set_mailbox(False)
+            c.close()
