@@ -49,8 +49,11 @@ public class GpuLogisticRegressionClassifier implements IClassifier {
         double reg = cfg ? 0.0 : 0.01;
         int d = fe.getFeatureDimension();
         weights = new double[d];
+        // :87 parallelize(epochs) under local[*]: one slice per available core, which fixes the
+        // per-iteration sample(false, frac, 42 + i) when frac < 1
+        int partitions = Runtime.getRuntime().availableProcessors();
         check(nativeTrain(CTX.get(), flatten(x, d), y, x.length, d, iters, step, reg, frac, 0.001,
-                          weights));
+                          partitions, weights));
     }
 
     @Override
@@ -93,7 +96,7 @@ public class GpuLogisticRegressionClassifier implements IClassifier {
     private static native long nativeCtxCreate(int device);
     private static native int nativeTrain(long ctx, double[] x, double[] y, int n, int d, int iters,
                                           double step, double reg, double frac, double tol,
-                                          double[] weights);
+                                          int partitions, double[] weights);
     private static native int nativePredict(long ctx, double[] x, int n, int d, double[] w,
                                             double[] out);
     private static native int nativeStatistics(double[] pred, double[] labels, int n, int[] out);

@@ -157,12 +157,13 @@ Java_cz_zcu_kiv_Classification_GpuLogisticRegressionClassifier_nativeCtxCreate(J
 JNIEXPORT jint JNICALL
 Java_cz_zcu_kiv_Classification_GpuLogisticRegressionClassifier_nativeTrain(
     JNIEnv* env, jclass k, jlong ctx, jdoubleArray x, jdoubleArray y, jint n, jint d, jint iters,
-    jdouble step, jdouble reg, jdouble frac, jdouble tol, jdoubleArray w) {
+    jdouble step, jdouble reg, jdouble frac, jdouble tol, jint partitions, jdoubleArray w) {
   (void)k;
   jdouble* px = PIN(x);
   jdouble* py = PIN(y);
   jdouble* pw = PIN(w);
-  const int rc = eegfx_shim_lr_train(ctx, px, py, n, d, iters, step, reg, frac, tol, pw);
+  const int rc = eegfx_shim_lr_train(ctx, px, py, n, d, iters, step, reg, frac, tol, partitions,
+                                     pw);
   UNPIN(w, pw, 0);
   UNPIN(y, py, JNI_ABORT);
   UNPIN(x, px, JNI_ABORT);

@@ -70,10 +70,11 @@ void eegfx_shim_odp_destroy(int64_t odp) { eegfx_odp_destroy((eegfx_odp*)(intptr
 
 int eegfx_shim_lr_train(int64_t ctx, const double* X, const double* y, int32_t n, int32_t d,
                         int32_t iterations, double step, double reg, double fraction, double tol,
-                        double* weights) {
+                        int32_t partitions, double* weights) {
   int32_t run = 0;
-  return eegfx_logreg_sgd_train((eegfx_ctx*)(intptr_t)ctx, X, y, n, d, iterations, step, reg,
-                                fraction, tol, weights, &run, EEGFX_MEM_HOST);
+  return eegfx_logreg_sgd_train_partitioned((eegfx_ctx*)(intptr_t)ctx, X, y, n, d, iterations,
+                                            step, reg, fraction, tol, partitions, weights, &run,
+                                            EEGFX_MEM_HOST);
 }
 
 int eegfx_shim_lr_predict(int64_t ctx, const double* X, int32_t n, int32_t d,

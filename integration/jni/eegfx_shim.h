@@ -57,10 +57,13 @@ int eegfx_shim_odp_get_features(int64_t odp, int32_t name, int32_t epoch_size, i
 void eegfx_shim_odp_destroy(int64_t odp);
 
 /* ---- GpuLogisticRegressionClassifier ------------------------------------------------------ */
-/* nativeTrain: MLlib LogisticRegressionWithSGD on the device (host arrays); weights in/out. */
+/* nativeTrain: MLlib LogisticRegressionWithSGD on the device (host arrays); weights in/out.
+ * partitions: the training RDD's partition count, which fixes Spark's per-iteration mini-batch
+ * sample when fraction < 1 -- parallelize(epochs) under local[*] makes defaultParallelism =
+ * Runtime.availableProcessors() slices (LogisticRegressionClassifier.java:87). */
 int eegfx_shim_lr_train(int64_t ctx, const double* X, const double* y, int32_t n, int32_t d,
                         int32_t iterations, double step, double reg, double fraction, double tol,
-                        double* weights);
+                        int32_t partitions, double* weights);
 /* nativePredict: LogisticRegressionModel.predict with the default threshold 0.5. */
 int eegfx_shim_lr_predict(int64_t ctx, const double* X, int32_t n, int32_t d,
                           const double* weights, double* out);

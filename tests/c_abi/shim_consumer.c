@@ -151,7 +151,7 @@ int main(int argc, char** argv) {
   /* GpuLogisticRegressionClassifier: train (the default constructor's parameters) and test */
   double wts[F];
   memset(wts, 0, sizeof wts);
-  CHECK(eegfx_shim_lr_train(ctx, feat, lab, (int32_t)n, F, 100, 1.0, 0.01, 1.0, 0.001, wts) ==
+  CHECK(eegfx_shim_lr_train(ctx, feat, lab, (int32_t)n, F, 100, 1.0, 0.01, 1.0, 0.001, 4, wts) ==
             EEGFX_OK,
         "train: %s", eegfx_last_error());
   double* pred = (double*)malloc(sizeof(double) * (size_t)n);
@@ -162,6 +162,14 @@ int main(int argc, char** argv) {
   printf("weights:");
   for (int j = 0; j < F; ++j) printf(" %a", wts[j]);
   printf("\nstatistics: %d %d %d %d\n", s[0], s[1], s[2], s[3]);
+  /* the config path with config_mini_batch_fraction = 0.5 (regParam 0.0, :98-108) over 4 slices */
+  memset(wts, 0, sizeof wts);
+  CHECK(eegfx_shim_lr_train(ctx, feat, lab, (int32_t)n, F, 20, 1.0, 0.0, 0.5, 0.001, 4, wts) ==
+            EEGFX_OK,
+        "train (mini-batch): %s", eegfx_last_error());
+  printf("weights_minibatch:");
+  for (int j = 0; j < F; ++j) printf(" %a", wts[j]);
+  printf("\n");
 
   eegfx_shim_odp_destroy(odp);
   CHECK(eegfx_shim_ctx_destroy(ctx) == EEGFX_OK, "ctx_destroy");
