@@ -4,7 +4,9 @@
 //
 //   hipcc ... -DFUSED_SRC='"build/v1/fused.hip"' window_probe.hip -o window_probe_v1
 //   PROBE_WIDE=1 PROBE_ITERS=2000 PROBE_EXACT=1 ./window_probe_v1
-//   PROBE_BASELINE=1: time the baseline kernel alone; PROBE_STEP=1: baseline + window per launch
+//   PROBE_BASELINE=1: time the baseline kernel alone; PROBE_STEP=1: baseline + window per launch;
+//   PROBE_FB=1 (built with -DPROBE_ONE_LAUNCH against history/one_launch_step_fused.patch): the
+//   step as one launch (launch_fused_step, window_fb_kernel)
 //   PROBE_N=8000000: another epoch count (one marker every 1,000 frames as always)
 //
 // Phase timestamps (per-workgroup s_memrealtime at each phase boundary):
@@ -80,8 +82,20 @@ int main() {
   (void)hipEventCreate(&b);
   const bool time_baseline = getenv("PROBE_BASELINE") != nullptr;
   const bool time_step = getenv("PROBE_STEP") != nullptr;  // baseline + window, as bench.py's step
+  // PROBE_FB=1: the step as one launch (window_fb_kernel, baselines folded in; built against
+  // history/one_launch_step_fused.patch with -DPROBE_ONE_LAUNCH)
+#ifdef PROBE_ONE_LAUNCH
+  const bool one_launch = getenv("PROBE_FB") != nullptr && !wide;
+  auto fstep = [&] {
+    (void)eegfx::launch_fused_step(0, raw, nf, ct, sel, ct, pos, n, fast, out, nullptr, g);
+  };
+#else
+  const bool one_launch = false;
+  auto fstep = [&] {};
+#endif
   auto one = [&] {
-    if (time_step) { baseline(); window(); }
+    if (one_launch) fstep();
+    else if (time_step) { baseline(); window(); }
     else if (time_baseline) baseline();
     else window();
   };
@@ -137,7 +151,9 @@ int main() {
     (void)hipFree(d_ts);
   }
 #endif
-  window();
+  (void)hipMemset(out, 0, n * 16 * ct * 8);
+  if (one_launch) fstep();
+  else { baseline(); window(); }
   std::vector<double> h(n * 16 * ct);
   (void)hipMemcpy(h.data(), out, h.size() * 8, hipMemcpyDeviceToHost);
   double s = 0, q = 0;
@@ -145,6 +161,6 @@ int main() {
   const hipError_t e = hipGetLastError();
   printf("%s %s %s: %.4f ms per launch (%d launches)  checksum %.17g %.17g  %s\n",
          wide ? "wide c32" : "window c3", fast ? "fma" : "exact",
-         time_step ? "step" : time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
+         one_launch ? "step-1-launch" : time_step ? "step" : time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
   return e == hipSuccess ? 0 : 1;
 }
