@@ -889,9 +889,10 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
 }
 
 // The opt-in resident form of the same path (eegfx_ctx_set_mailbox): one workgroup that stays on
-// the device and serves the context's small host batches without a launch each.  Thread 0 polls
-// the request word of a host-mapped MailboxCmd (system-scope atomic loads, a short s_sleep between
-// polls); a new request's epochs are read from its pinned rows, computed by small_epoch exactly as
+// the device and serves the context's small host batches without a launch each.  Wave 0 polls
+// the 64-bit request word of a host-mapped MailboxCmd (system-scope atomic loads, a short s_sleep
+// between polls; the word carries the sequence number and the whole request); a new request's
+// epochs are read from its pinned rows, computed by small_epoch exactly as
 // features_small_kernel does, and written to its pinned output, then the completed sequence
 // number is published (system-scope release after every wave's stores).  The kernel returns when
 // the host sets `stop`, or after idle_ticks (s_memrealtime, 100 MHz) without a request -- every
