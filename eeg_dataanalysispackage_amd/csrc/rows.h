@@ -75,7 +75,10 @@ __device__ __forceinline__ void normalise_store(double* fb, double* norm, double
       for (uint64_t f = flagged; f; f &= f - 1) {
         const int e1 = __ffsll((unsigned long long)f) - 1;
         const double acc_e = lane_value(acc, e1);  // e1 is wave-uniform
-        if (guard_fails(acc_e, kGuardK2Collapsed, recheck(e1 >> 3))) left |= 1ull << e1;
+        // the verdict is wave-uniform: a scalar branch keeps `left` in SGPRs
+        if (__builtin_amdgcn_readfirstlane(
+                guard_fails(acc_e, kGuardK2Collapsed, recheck(e1 >> 3)) ? 1 : 0))
+          left |= 1ull << e1;
       }
       if (lane == 0) {
         guard_count_rechecked(g, __popcll(flagged));
