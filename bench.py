@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--spacing", type=int, default=FRAMES_PER_EPOCH,
                     help="c3/c32: frames between markers (default 1000, the headline; < 687 makes "
                          "windows overlap and the window DMA cached instead of streaming)")
+    ap.add_argument("--lib", default=None,
+                    help="study only: another build of libeegfx.so to load (A/B of library builds)")
     ap.add_argument("--numerics", choices=["exact", "fma"], default="fma",
                     help="fma: fused filter bank (<=1e-9 of the reference, the north_star bound); "
                          "exact: the reference's operation order, bit-identical")
@@ -249,6 +251,9 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    if args.lib:
+        from eeg_dataanalysispackage_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     import eeg_dataanalysispackage_amd as fx
 
     if args.workload == "stream":

@@ -325,9 +325,11 @@ struct eegfx_ctx {
   void tic() {
     if (!timing) return;
     if (n_timed == events.size()) {
+      // timing only (read after the stream drains): no system-scope fence at each record, so
+      // the bracketed kernel's neighbours pay no cache writeback / invalidate for the timing
       hipEvent_t a, b;
-      HIP_CHECK(hipEventCreate(&a));
-      HIP_CHECK(hipEventCreate(&b));
+      HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+      HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
       events.emplace_back(a, b);
       event_bytes.push_back(0);
     }
