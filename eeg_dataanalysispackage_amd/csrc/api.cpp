@@ -231,8 +231,7 @@ struct eegfx_ctx {
     // the staging a server reads is fixed for its lifetime (growing it stops the server first)
     mb_host->rows = pin_in.p ? (const double*)pin_in.device_ptr() : nullptr;
     mb_host->out = pin_out.p ? (double*)pin_out.device_ptr() : nullptr;
-    const Guard g{guard_dev, nullptr, guard_recomputed_slots(), guard_rechecked_slots()};
-    HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks, g));
+    HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks));
     mb_live = true;
   }
   void mb_stop() {
@@ -268,8 +267,7 @@ struct eegfx_ctx {
     const auto now = std::chrono::steady_clock::now();
     // the kernel returns after 1 s without a request: relaunch it when it may have
     if (!mb_live || (now - mb_last > std::chrono::milliseconds(500) && mb_returned())) mb_launch();
-    __atomic_store_n(&m->req, mailbox_request(mb_seq, numerics != EEGFX_EXACT, C, nfeat, n),
-                     __ATOMIC_RELEASE);
+    __atomic_store_n(&m->req, mailbox_request(mb_seq, C, nfeat, n), __ATOMIC_RELEASE);
     for (uint64_t spin = 1;; ++spin) {
       if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == mb_seq) break;
       if ((spin & 4095) == 0) {
@@ -945,7 +943,8 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         // packed into a pinned, device-mapped buffer by the calling thread and the kernel
         // (features_small_kernel) reads them -- and writes the rows -- across the host link
         // directly: one launch and one stream sync, no DMA transfers (each costs a copy-engine
-        // round trip) and no allocation once the context's staging has grown.
+        // round trip) and no allocation once the context's staging has grown.  The rows are EXACT
+        // under both numerics (kernels.hip small_epoch), so the fma guard does not count them.
         // growing a pinned buffer frees the old one, which synchronises the device: stop the
         // resident server first (the next request restarts it)
         if (ctx->mailbox && ((size_t)n * C * row_w > ctx->pin_in.cap || out_bytes > ctx->pin_out.cap))
@@ -954,16 +953,17 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         double* hout = (double*)ctx->pin_out.get(out_bytes);
         for (int64_t r = 0; r < n * C; ++r)
           memcpy((uint8_t*)hin + (size_t)r * row_w, src + (size_t)r * row_p, row_w);
-        if (ctx->mailbox) {  // the resident server: no launch, no stream sync
-          (void)ctx->guard_for(n);
+        // The resident server (no launch, no stream sync) takes single epochs: it serves a
+        // request's epochs one after another (~7 us each), where a launch runs them on a
+        // workgroup each (11 epochs: ~20 us launched against ~80 us served).
+        if (ctx->mailbox && n == 1) {
           ctx->mb_serve(n, C, feature_size);
           memcpy(out, hout, out_bytes);
           return;
         }
         ctx->tic();
         HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
-                                        feature_size, ctx->numerics != EEGFX_EXACT,
-                                        (double*)ctx->pin_out.device_ptr(), ctx->guard_for(n)));
+                                        feature_size, (double*)ctx->pin_out.device_ptr()));
         ctx->toc(0);
         ctx->wait_small();
         ctx->check_positions_flag();

@@ -544,6 +544,63 @@ __device__ __forceinline__ double rsqrt_nr(double v) {
   return r;
 }
 
+// One level of the analysis low-pass over a whole wave under EXACT numerics: out[i] =
+// fir10(in[2i .. 2i + 9] mod N) for i < N / 2, lane l computing outputs l, l + 64, ...  The ten
+// inputs are read as five 16-byte LDS pairs (2i and every pair offset are even, so no pair wraps).
+template <int N>
+__device__ __forceinline__ void level_wave(const double* in, double* out, int lane) {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  constexpr int H = N / 2;
+#pragma unroll
+  for (int i0 = 0; i0 < H; i0 += 64) {
+    const int i = i0 + lane;
+    if (H >= 64 || i < H) {
+      double x[kTaps];
+#pragma unroll
+      for (int t = 0; t < kTaps / 2; ++t) {
+        const f64x2 p = *(const f64x2*)(in + ((2 * i + 2 * t) & (N - 1)));
+        x[2 * t] = p.x;
+        x[2 * t + 1] = p.y;
+      }
+      out[i] = fir10<false, false>(x);
+    }
+  }
+}
+
+// The six levels of one signal by one wave under EXACT numerics (the per-epoch path, small_epoch):
+// each level's outputs spread over the 64 lanes (4, 2, 1 per lane at levels 1-3, then 32 and 16
+// lanes), every output the reference's sum in its order (WaveletTransform.java:126-137, the
+// eegdsp DWT of SURVEY.md Appendix A: one rounded multiply and one rounded add per tap in j order,
+// -ffp-contract=off; fir10 as in the other EXACT paths).
+// x: the 512 window doubles in LDS (16-byte aligned); scratch: 384 doubles of this wave's LDS
+// (16-byte aligned), levels ping-pong through it.  Returns feature `lane` of the signal: a6[lane]
+// on lanes 0-7, d6[lane - 8] on lanes 8-15, 0 elsewhere.  A one-epoch call is latency-bound on one
+// workgroup, and this form's per-lane chain is ~190 operations against the 8-lanes-per-signal
+// cascade's ~1,200.
+__device__ __forceinline__ double dwt8_exact_signal_wave(const double* x, double* scratch,
+                                                         int lane) {
+  level_wave<512>(x, scratch, lane);
+  wave_sync();
+  level_wave<256>(scratch, scratch + 256, lane);
+  wave_sync();
+  level_wave<128>(scratch + 256, scratch, lane);
+  wave_sync();
+  level_wave<64>(scratch, scratch + 256, lane);
+  wave_sync();
+  level_wave<32>(scratch + 256, scratch, lane);
+  wave_sync();
+  double f = 0.0;
+  if (lane < 16) {  // level 6 on the 16 values of a5
+    const int i = lane & 7;
+    double v[kTaps];
+#pragma unroll
+    for (int j = 0; j < kTaps; ++j) v[j] = scratch[(2 * i + j) & 15];
+    f = lane < 8 ? fir10<false, false>(v) : fir10<false, true>(v);
+  }
+  wave_sync();  // scratch is free for the wave's next signal
+  return f;
+}
+
 // One feature row under EXACT numerics by one wave, for the rare rows the fma numerics'
 // conditioning guard cannot certify (guard.h): for each of the C channels the 512 window samples
 // (sample(c, k): the decoded doubles) go to LDS, the six levels run with every output

@@ -766,33 +766,34 @@ __global__ __launch_bounds__(64) void features_from_epochs_kernel(const double* 
 // epoch reads the epoch's packed window rows (C x 512 doubles, pinned host memory mapped into the
 // device) with 16-byte loads, all issued before the first wait -- one host-link round trip instead
 // of the 72 dependent-free but scattered 8-byte loads per lane of features_from_epochs_kernel --
-// stages them in LDS, runs the filter bank (wave = 8 channels x 8 segments), normalises, and
-// writes the row back across the link.  C <= kSmallMaxC.
+// stages them in LDS, runs each channel's six levels on a whole wave (dwt8_exact_signal_wave,
+// channels dealt over the four waves), normalises, and writes the row back across the link.
+// C <= kSmallMaxC.
+//
+// One epoch on one workgroup is a latency problem, not a throughput one, so this path computes
+// EXACT numerics under both settings: the whole-wave levels keep each lane's dependent chain short
+// (~190 operations) where the batch kernels' 8-lanes-per-signal fma cascade runs ~1,200 per lane,
+// and an EXACT row needs no conditioning guard.  Under fma numerics the rows are therefore the
+// EXACT ones (inside the 1e-9 contract by definition); the guard's counters do not count them.
 constexpr int kSmallMaxC = 16;
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
-#error "features_small_kernel stages 66 KB of LDS per workgroup: gfx950 (160 KB per CU) only"
+#error "features_small_kernel stages 80 KB of LDS per workgroup: gfx950 (160 KB per CU) only"
 #endif
-static_assert(sizeof(double) * (kSmallMaxC * kWin + kSmallMaxC * 16 + 1) <= 160 * 1024,
-              "features_small_kernel's LDS exceeds one gfx950 CU");
-// Under fma numerics the row is checked against the conditioning guard (guard.h, measured X per
-// channel); a failing row is recomputed right here with the EXACT cascade from the staged windows
-// (no follow-up launch on this latency-bound path), and counted in the guard's running total.
 struct SmallLds {
   double xs[kSmallMaxC * kWin];
+  double scr[4][384];  // per-wave level scratch (dwt8_exact_signal_wave)
   double feat[kSmallMaxC * 16];
-  double gx[kSmallMaxC];
   double norm;
-  int redo;
 };
+static_assert(sizeof(SmallLds) <= 160 * 1024, "features_small_kernel's LDS exceeds one gfx950 CU");
 
 // One epoch (its C x 512 window doubles at `src`, 16-byte aligned) -> its row at `dst`, by a
 // workgroup of 256 threads (uniform control flow; ends with a barrier).
-template <bool FAST>
 __device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows, int C, int nfeat,
-                                            double* __restrict__ dst, const Guard& guard,
-                                            SmallLds& sh) {
+                                            double* __restrict__ dst, SmallLds& sh) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const f64x2* src = (const f64x2*)src_rows;
   const int npairs = C * kWin / 2;  // <= 4096: at most 16 per thread
   f64x2 v[16];
@@ -808,38 +809,15 @@ __device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows,
   }
   __syncthreads();
   const int F = C * nfeat;
-  const int s = lane & 7;
-  auto bank = [&](auto fast_tag) {
-    constexpr bool FA = decltype(fast_tag)::value;
-    for (int c0 = 8 * w; c0 < C; c0 += 32) {  // uniform per wave
-      const int c = c0 + (lane >> 3);
-      const bool valid = c < C;
-      const double* xr = sh.xs + (valid ? c : 0) * kWin;
-      double x[kIn];
-#pragma unroll
-      for (int k = 0; k < kIn; ++k) x[k] = xr[(kSegLen * s + k) & (kWin - 1)];
-      double a6, d6;
-      dwt8_cascade<FA, true>(x, nullptr, lane & ~7, s, a6, d6);
-      if constexpr (FA) {  // the guard's X: max |x| over the lane's own 64 samples, then the group
-        double xm = 0.0;
-#pragma unroll
-        for (int k = 0; k < kSegLen; ++k) xm = fmax(xm, fabs(x[k]));
-        xm = group8_max(xm);
-        if (valid && s == 0) sh.gx[c] = xm * xm;
-      }
-      if (valid) {
-        if (s < nfeat) sh.feat[c * nfeat + s] = a6;
-        if (8 + s < nfeat) sh.feat[c * nfeat + 8 + s] = d6;
-      }
-    }
-    __syncthreads();
-  };
-  if constexpr (FAST) bank(std::true_type{});
-  else bank(std::false_type{});
+  for (int c = w; c < C; c += 4) {  // uniform per wave
+    const double f = dwt8_exact_signal_wave(sh.xs + c * kWin, sh.scr[w], lane);
+    if (lane < nfeat) sh.feat[c * nfeat + lane] = f;
+  }
+  __syncthreads();
   // SignalProcessing.normalize: Math.pow(f, 2) summed in index order.  Wave 0 squares 64
   // features at a time, one per lane, and the running sum walks the lanes in order (readlane),
   // so the additions are the reference's, in its order, without a serial LDS round trip each.
-  auto sum_squares = [&]() {
+  if (w == 0) {
     double acc = 0.0;
     for (int base = 0; base < F; base += 64) {
       const int i = base + lane;
@@ -847,45 +825,19 @@ __device__ __forceinline__ void small_epoch(const double* __restrict__ src_rows,
       const int m = F - base < 64 ? F - base : 64;
       for (int j = 0; j < m; ++j) acc = acc + lane_value(sq, j);
     }
-    return acc;
-  };
-  if (w == 0) {  // uniform per wave
-    const double acc = sum_squares();
-    if (lane == 0) {
-      sh.norm = sqrt(acc);
-      sh.redo = 0;
-      if (FAST && guard.total) {
-        double sx = 0.0;
-        for (int c = 0; c < C; ++c) sx += sh.gx[c];
-        sh.redo = guard_fails(acc, kGuardK2Cascade, sx) ? 1 : 0;
-      }
-    }
+    if (lane == 0) sh.norm = sqrt(acc);
   }
   __syncthreads();
-  if (FAST && sh.redo) {  // uniform: the EXACT filter bank and normalisation on the staged windows
-    bank(std::false_type{});
-    if (w == 0) {
-      const double acc = sum_squares();
-      if (lane == 0) {
-        sh.norm = sqrt(acc);
-        guard_count_recomputed(guard, 1ull);
-      }
-    }
-    __syncthreads();
-  }
   for (int i = tid; i < F; i += 256) dst[i] = sh.feat[i] / sh.norm;
   __syncthreads();  // sh is reused by the next epoch
 }
 
-template <bool FAST>
 __global__ __launch_bounds__(256) void features_small_kernel(const double* __restrict__ rows,
-                                                             int64_t n, int C, int nfeat,
-                                                             double* __restrict__ out,
-                                                             Guard guard) {
+                                                             int C, int nfeat,
+                                                             double* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) SmallLds sh;
   const int64_t e = blockIdx.x;
-  (void)n;
-  small_epoch<FAST>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, guard, sh);
+  small_epoch(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, sh);
 }
 
 // The opt-in resident form of the same path (eegfx_ctx_set_mailbox): one workgroup that stays on
@@ -897,8 +849,7 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
 // number is published (system-scope release after every wave's stores).  The kernel returns when
 // the host sets `stop`, or after idle_ticks (s_memrealtime, 100 MHz) without a request -- every
 // wave reaches that exit; the host relaunches it on the next request.
-__global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, uint64_t idle_ticks,
-                                                               Guard guard) {
+__global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, uint64_t idle_ticks) {
   __shared__ __attribute__((aligned(16))) SmallLds sh;
   __shared__ uint32_t cmd[2];  // request to serve, 0 = return
   const int tid = threadIdx.x;
@@ -939,18 +890,12 @@ __global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, u
     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)cmd[0]);
     if (seq == 0) break;  // stop or idle
     const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane((int)cmd[1]);
-    const int fast = (int)(word >> 31);
     const int C = (int)((word >> 26) & 31) + 1, nfeat = (int)((word >> 21) & 31) + 1;
     const int64_t n = (int64_t)(word & ((1u << 21) - 1));
     // every wave: no stale line of the (reused) pinned rows from an earlier request
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    if (fast)
-      for (int64_t e = 0; e < n; ++e)
-        small_epoch<true>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, guard, sh);
-    else
-      for (int64_t e = 0; e < n; ++e)
-        small_epoch<false>(rows + e * C * kWin, C, nfeat, out + e * C * nfeat,
-                           Guard{nullptr, nullptr, nullptr}, sh);
+    for (int64_t e = 0; e < n; ++e)
+      small_epoch(rows + e * C * kWin, C, nfeat, out + e * C * nfeat, sh);
     __threadfence_system();  // this thread's rows reach the host before the flag below
     __syncthreads();
     if (tid == 0) __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1164,22 +1109,17 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
 
 bool features_small_supported(int C) { return C >= 1 && C <= dev::kSmallMaxC; }
 
-hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
-                                   const Guard& guard) {
-  hipLaunchKernelGGL(dev::features_mailbox_kernel, dim3(1), dim3(256), 0, st, mb, idle_ticks, guard);
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks) {
+  hipLaunchKernelGGL(dev::features_mailbox_kernel, dim3(1), dim3(256), 0, st, mb, idle_ticks);
   return hipGetLastError();
 }
 
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
-                                 bool fast, double* out, const Guard& guard) {
+                                 double* out) {
   if (n == 0) return hipSuccess;
   if (!features_small_supported(C)) return hipErrorNotSupported;
-  if (fast)
-    hipLaunchKernelGGL(dev::features_small_kernel<true>, dim3((unsigned)n), dim3(256), 0, st, rows,
-                       n, C, nfeat, out, guard);
-  else
-    hipLaunchKernelGGL(dev::features_small_kernel<false>, dim3((unsigned)n), dim3(256), 0, st, rows,
-                       n, C, nfeat, out, Guard{nullptr, nullptr, nullptr});
+  hipLaunchKernelGGL(dev::features_small_kernel, dim3((unsigned)n), dim3(256), 0, st, rows, C,
+                     nfeat, out);
   return hipGetLastError();
 }
 

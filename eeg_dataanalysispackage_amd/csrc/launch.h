@@ -48,9 +48,10 @@ bool features_small_supported(int C);
 // The resident small-batch server (eegfx_ctx_set_mailbox): a host-mapped command block, written
 // by the host except `done` (the device's last completed request).
 struct MailboxCmd {
-  // The request word, written last by the host (release): sequence number << 32 | fast << 31 |
-  // (C - 1) << 26 | (nfeat - 1) << 21 | n -- the whole request in one aligned 64-bit load, so the
-  // kernel needs no second round trip across the host link for its fields.
+  // The request word, written last by the host (release): sequence number << 32 | (C - 1) << 26 |
+  // (nfeat - 1) << 21 | n -- the whole request in one aligned 64-bit load, so the kernel needs no
+  // second round trip across the host link for its fields (bit 31 unused: the per-epoch path
+  // computes EXACT rows under both numerics).
   uint64_t req;
   uint32_t done;  // the last sequence number whose rows are in `out` (device)
   uint32_t stop;  // 1: the kernel returns
@@ -58,14 +59,13 @@ struct MailboxCmd {
   const double* rows;  // device-mapped pinned [n][C][512] window doubles
   double* out;         // device-mapped pinned [n][C * nfeat] rows
 };
-inline uint64_t mailbox_request(uint32_t seq, bool fast, int C, int nfeat, int64_t n) {
-  return (uint64_t)seq << 32 | (uint64_t)(fast ? 1 : 0) << 31 | (uint64_t)(C - 1) << 26 |
-         (uint64_t)(nfeat - 1) << 21 | (uint64_t)n;
+inline uint64_t mailbox_request(uint32_t seq, int C, int nfeat, int64_t n) {
+  return (uint64_t)seq << 32 | (uint64_t)(C - 1) << 26 | (uint64_t)(nfeat - 1) << 21 |
+         (uint64_t)n;
 }
-hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
-                                   const Guard& guard);
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks);
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
-                                 bool fast, double* out, const Guard& guard);
+                                 double* out);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);
 
 // Non-temporal reads pay when the regions neighbouring epochs read do not overlap: the average

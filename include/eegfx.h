@@ -38,6 +38,8 @@
  * conditioning guard bounds each row's rounding difference from the EXACT row,
  * and the rows it cannot certify (features at rounding level, e.g. a window in the filters' null
  * space) are recomputed under EXACT on the device before the call's results are complete.
+ * Small host batches of eegfx_extract_features_f64 (the per-epoch drop-in) are computed under
+ * EXACT in both settings (latency-bound; the guard's counters do not count them).
  */
 #ifndef EEGFX_H_
 #define EEGFX_H_
@@ -124,10 +126,10 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
                            int64_t* rows_recomputed, int reset);
 /* Opt-in resident server for the per-epoch drop-in (IFeatureExtraction.extractFeatures called
  * once per epoch, LogisticRegressionClassifier.java:55-61): enable != 0 starts one resident
- * workgroup on its own stream that polls a host-mapped command word, so small EEGFX_MEM_HOST
- * eegfx_extract_features_f64 batches on this context (<= 768 KB of window rows, C <= 16) are
- * served without a kernel launch or a stream synchronisation -- the same kernel code, the same
- * rows.  It returns by itself after 1 s without a request (and is restarted by the next one), or
+ * workgroup on its own stream that polls a host-mapped command word, so single-epoch
+ * EEGFX_MEM_HOST eegfx_extract_features_f64 calls on this context (C <= 16) are served without a
+ * kernel launch or a stream synchronisation -- the same device code, the same rows (small
+ * batches of more epochs stay on the launch path, which runs them in parallel).  It returns by itself after 1 s without a request (and is restarted by the next one), or
  * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
  * (hipDeviceSynchronize) waits for it: disable it before such calls.  Off by default. */
 int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable);
