@@ -66,8 +66,10 @@ struct DevBuf {
 };
 
 // Grow-only pinned host buffer (hipHostMalloc: mapped into the device address space), for the
-// small-batch IFeatureExtraction path.  Only touched by the owning context's calls, which
-// synchronise before they return.
+// small-batch IFeatureExtraction path and the streamed path's host staging.  Only touched by the
+// owning context's calls, which synchronise before they return.  Kept across calls: hipHostFree
+// synchronises the whole device, which waits for any context's resident server (up to its 1 s
+// idle exit), so a buffer is freed only when it grows and when the context is destroyed.
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -153,6 +155,7 @@ struct eegfx_ctx {
   DevBuf raw, pos, out, scratch, fused;
   DevBuf lr_x, lr_y, lr_state, lr_part, lr_mask;  // logistic regression (eegfx_logreg_*)
   PinBuf pin_in, pin_out;                // small-batch extract_features staging (zero-copy)
+  PinBuf pin_chunk[2];                   // streamed path: host staging of pageable recordings
   // The fma numerics' conditioning guard (guard.h): device memory holding the flagged-row count
   // of the current window_wide_kernel launch (first 128 B), then the running totals of recomputed
   // rows and of rows that went to the second stage, each spread over kGuardSlots lines; the
@@ -184,6 +187,8 @@ struct eegfx_ctx {
       b->release();
     pin_in.release();
     pin_out.release();
+    pin_chunk[0].release();
+    pin_chunk[1].release();
   }
   // streamed path (eegfx_process_recording_streamed): upload / download streams and the chunk
   // events, created on first use and kept for the context's lifetime
@@ -777,7 +782,13 @@ int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable) {
     if (ctx->mailbox) return;
     ctx->mailbox = true;  // from here on release_mailbox undoes whatever was set up
     try {
-      HIP_CHECK(hipStreamCreateWithFlags(&ctx->mb_stream, hipStreamNonBlocking));
+      // A stream of the highest priority: the runtime multiplexes a process's streams of one
+      // priority over a few hardware queues (4 here), and a queue runs its packets in order, so
+      // a normal-priority stream sharing the resident kernel's queue would wait behind it (up to
+      // its 1 s idle exit).  The high-priority pool keeps the server on a queue of its own.
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_CHECK(hipStreamCreateWithPriority(&ctx->mb_stream, hipStreamNonBlocking, greatest));
       HIP_CHECK(hipHostMalloc((void**)&ctx->mb_host, sizeof(MailboxCmd),
                               hipHostMallocMapped | hipHostMallocCoherent));
       memset(ctx->mb_host, 0, sizeof(MailboxCmd));
@@ -1133,10 +1144,6 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
     hipStream_t cs = ctx->up, os = ctx->down;  // upload (H2D) and download (D2H) streams
     hipEvent_t* copied = ctx->copied;
     hipEvent_t* done = ctx->done;
-    auto cleanup = [&] {
-      for (int b = 0; b < 2; ++b)
-        if (pin[b]) (void)hipHostFree(pin[b]);
-    };
     // Chunk sizes ramp up (c/4, c/2, then c) and down (about half of what remains, not below
     // c/4) so that the first upload and the last download -- the parts of a call that nothing
     // overlaps -- stay short.
@@ -1148,8 +1155,11 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       return std::min(chunk_frames, std::max(c, std::max(chunk_frames / 4, 2 * kSpan)));
     };
     try {
-      for (int b = 0; b < 2; ++b)
-        if (!pinned) HIP_CHECK(hipHostMalloc(&pin[b], cbytes, hipHostMallocDefault));
+      if (!pinned) {  // the context's grow-only staging (a growth frees: stop our server first)
+        if (ctx->mailbox && cbytes > std::min(ctx->pin_chunk[0].cap, ctx->pin_chunk[1].cap))
+          ctx->mb_stop();
+        for (int b = 0; b < 2; ++b) pin[b] = ctx->pin_chunk[b].get(cbytes);
+      }
       ctx->drain();  // d_pos uploaded; buffers idle
       int64_t i = 0, k = 0;
       while (i < n) {
@@ -1203,10 +1213,8 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       (void)hipStreamSynchronize(ctx->stream);
       if (cs) (void)hipStreamSynchronize(cs);
       if (os) (void)hipStreamSynchronize(os);
-      cleanup();
       throw;
     }
-    cleanup();
   });
 }
 

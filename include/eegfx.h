@@ -131,7 +131,10 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
  * kernel launch or a stream synchronisation -- the same device code, the same rows (small
  * batches of more epochs stay on the launch path, which runs them in parallel).  It returns by itself after 1 s without a request (and is restarted by the next one), or
  * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
- * (hipDeviceSynchronize) waits for it: disable it before such calls.  Off by default. */
+ * (hipDeviceSynchronize, hipFree, hipHostFree) waits for it: disable it before such calls.  Its
+ * stream has the highest priority, which keeps it on a hardware queue of its own (streams of one
+ * priority share a few queues in order); batches launched on the same context meanwhile take
+ * ~30 us longer.  Off by default. */
 int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
@@ -248,7 +251,8 @@ int eegfx_process_recording_epochs(eegfx_ctx* ctx, const void* raw, int32_t fmt,
  * n_channels_total samples), pos and features are HOST arrays; the recording is moved to the device
  * in chunks of at most chunk_frames frames (>= 787, the frames one epoch spans) on an upload
  * stream that runs up to three chunks ahead of the kernels (a ring of four device chunk buffers;
- * pageable sources go through two pinned staging buffers, pinned sources are copied directly),
+ * pageable sources go through two pinned staging buffers that the context keeps for later calls
+ * and frees when it is destroyed, pinned sources are copied directly),
  * and the rows of each chunk return on a download stream.  Positions may come in any
  * order; features[i] belongs to pos[i].  Results equal eegfx_process_recording on the whole
  * recording (bit for bit under EEGFX_EXACT).  Replaces the whole-file readBinaryData decode of

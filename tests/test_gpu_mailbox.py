@@ -122,3 +122,37 @@ def test_per_epoch_kernel_any_channel_count(C, nfeat):
         finally:
             c.set_mailbox(False)
             c.close()
+
+
+def test_streamed_calls_beside_resident_servers(epochs):
+    """The streamed ingest on a context whose server -- and another context's -- is resident: its
+    pinned staging is grow-only, so a call neither frees host memory (hipHostFree synchronises the
+    whole device, i.e. waits up to 1 s for every resident server's idle exit) nor returns wrong
+    rows; growth stops the context's own server first."""
+    rng = np.random.default_rng(5)
+    nf = 40_000
+    raw = np.clip(-25000 + np.cumsum(rng.integers(-40, 41, size=(nf, 3)), axis=0), -32768,
+                  32767).astype(np.int16)
+    pos = np.arange(1000, nf - 1000, 997, dtype=np.int64)
+    want = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
+    want_ep = oracle.extract_features(epochs[:1])
+    c, other = fx.Context(0), fx.Context(0)
+    try:
+        for x in (c, other):
+            x.set_mailbox(True)
+            assert eq(x.extract_features(epochs[:1]), want_ep)
+        times = []
+        for chunk in (5000, 5000, 9000):   # first use, reuse, growth
+            t = time.perf_counter()
+            got = c.process_recording_streamed(raw, 3, [0, 1, 2], [0.1] * 3, pos,
+                                               chunk_frames=chunk)
+            times.append(time.perf_counter() - t)
+            assert eq(got, want), chunk
+            assert eq(other.extract_features(epochs[:1]), want_ep)   # other's server still serves
+        print("streamed call times (first use, reuse, growth):", times)
+        assert times[1] < 0.5, times   # reuse: no device-wide synchronisation behind the servers
+        assert eq(c.extract_features(epochs[:1]), want_ep)   # c's server restarted after growth
+    finally:
+        for x in (c, other):
+            x.set_mailbox(False)
+            x.close()

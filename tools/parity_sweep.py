@@ -8,6 +8,8 @@ legal edges (pos = 100, windows past the end, pos - 100 = n_frames), then
   * eegfx_process_recording (host and device buffers), both numerics,
   * eegfx_process_recording_epochs (epochs + features in one pass), both numerics,
   * eegfx_extract_features_f64 on the oracle's epochs with a random feature size and skip,
+    on device epochs and (C <= 16) on host epochs through the per-epoch kernel: up to 4 epochs,
+    one epoch under fma, one epoch served by a context's resident server (eegfx_ctx_set_mailbox),
   * every fifth case, eegfx_process_recording_streamed with a random chunk size (EXACT).
 EXACT must equal the oracle value for value (epochs always); fma within 1e-9 per feature.
 
@@ -16,6 +18,7 @@ held samples (flat, the value at pos-100) or zeros (silent): the rows the fma gu
 stage flags and its second stage certifies (the guard counters are added to the summary).
 
   python tools/parity_sweep.py [--cases 2000] [--seed0 0] [--flat] [--out summary.json]
+                               [--max-seconds S]
 """
 import argparse
 import json
@@ -65,11 +68,15 @@ def main():
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--flat", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--max-seconds", type=float, default=0.0,
+                    help="stop after this long (the summary counts the cases run)")
     a = ap.parse_args()
     import torch
     import eeg_dataanalysispackage_amd as fx
     from oracle import oracle
     ex, fm = fx.Context(0, numerics="exact"), fx.Context(0, numerics="fma")
+    mb = fx.Context(0)  # host calls only: the per-epoch resident server
+    mb.set_mailbox(True)
     fm.guard_detail(reset=True)
     stats = {"cases": 0, "epochs": 0, "checks": 0, "mismatches": [], "max_fma_err": 0.0,
              "by_channels": {}}
@@ -84,6 +91,8 @@ def main():
         return err <= 1e-9, err
 
     for seed in range(a.seed0, a.seed0 + a.cases):
+        if a.max_seconds and time.time() - t0 > a.max_seconds:
+            break
         raw, ct, cols, res, pos, nfeat, skip = case(seed, a.flat)
         want = oracle.process_recording(raw, cols, res, pos)
         want_ep = oracle.decode_epochs(raw, cols, res, pos)
@@ -120,6 +129,19 @@ def main():
         ok, err3 = fma_ok(fm.extract_features(dep, feature_size=nfeat, skip=skip).cpu().numpy(),
                           want_x)
         results.append(("extract_features fma device", ok, err3))
+        if len(cols) <= 16:  # host epochs: the per-epoch kernel (features_small_kernel)
+            k = min(len(pos), 4)
+            results.append(("extract_features exact host small",
+                            np.array_equal(ex.extract_features(want_ep[:k], feature_size=nfeat,
+                                                               skip=skip),
+                                           want_x[:k], equal_nan=True), 0.0))
+            ok, err4 = fma_ok(fm.extract_features(want_ep[:1], feature_size=nfeat, skip=skip),
+                              want_x[:1])
+            results.append(("extract_features fma host single", ok, err4))
+            results.append(("extract_features resident server",
+                            np.array_equal(mb.extract_features(want_ep[-1:], feature_size=nfeat,
+                                                               skip=skip),
+                                           want_x[-1:], equal_nan=True), 0.0))
         stats["cases"] += 1
         stats["epochs"] += len(pos)
         key = str(len(cols))
@@ -139,6 +161,8 @@ def main():
                       "rows_recomputed": recomputed, "flat": a.flat}
     ex.close()
     fm.close()
+    mb.set_mailbox(False)
+    mb.close()
     stats["seconds"] = round(time.time() - t0, 1)
     stats["mismatches"] = stats["mismatches"][:20]
     line = json.dumps(stats)
