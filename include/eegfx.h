@@ -133,8 +133,7 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
  * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
  * (hipDeviceSynchronize, hipFree, hipHostFree) waits for it: disable it before such calls.  Its
  * stream has the highest priority, which keeps it on a hardware queue of its own (streams of one
- * priority share a few queues in order); batches launched on the same context meanwhile take
- * ~30 us longer.  Off by default. */
+ * priority share a few queues in order).  Off by default. */
 int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
