@@ -868,16 +868,18 @@ __global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, u
       uint64_t go = 0;
       const uint64_t t0 = wall_clock64();
       for (;;) {
-        const uint64_t r = __hip_atomic_load(&mb->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // both words in one round trip across the link: relaxed loads issued back to back (an
+        // acquire load would wait for its value before the second load); the acquire is the
+        // system-scope fence every wave runs once a request is seen
+        const uint64_t r = __hip_atomic_load(&mb->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t st = __hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(r >> 32));
         if (hi != last) {
           go = (uint64_t)hi << 32 | lo;
           break;
         }
-        if (__builtin_amdgcn_readfirstlane(
-                (int)__hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)))
-          break;
+        if (__builtin_amdgcn_readfirstlane((int)st)) break;
         if (wall_clock64() - t0 > idle_ticks) break;
         __builtin_amdgcn_s_sleep(2);
       }
