@@ -7,20 +7,25 @@ import org.apache.commons.logging.Log;
 import org.apache.commons.logging.LogFactory;
 
 /**
- * OffLineDataProvider (OffLineDataProvider.java:42-380) on an MI355X: the same constructor,
- * loadData, getData and getDataLabels, plus getFeatures -- the rows of WaveletTransform(8, 512,
- * 175, 16) for every epoch in getData() order, which loadData computes in the same pass over each
- * epoch's frames (eegfx_odp_load_data -> eegfx_process_recording_epochs), so getFeatures is a copy
- * of rows that already exist.  Local files only (the reference's HDFS client is out of scope).
+ * OffLineDataProvider (OffLineDataProvider.java:42-380) on an MI355X, as a subclass: a caller that
+ * holds the provider as an OffLineDataProvider (PipelineBuilder.java:115-120, the
+ * OfflineDataProviderTest cases) changes only its `new`.  The constructor keeps the reference's
+ * signature (`throws Exception`, :78); loadData, getData and getDataLabels are overridden (:88,
+ * :370, :377), so the base class's HDFS client (:90) is never reached.  getFeatures adds the rows
+ * of WaveletTransform(8, 512, 175, 16) for every epoch in getData() order, which loadData computes
+ * in the same pass over each epoch's frames (eegfx_odp_load_data ->
+ * eegfx_process_recording_epochs), so it is a copy of rows that already exist.  Local files only
+ * (the reference's HDFS client is out of scope).
  */
-public class GpuOffLineDataProvider {
+public class GpuOffLineDataProvider extends OffLineDataProvider {
     static { System.loadLibrary("eegfx_jni"); }
 
     private static final Log logger = LogFactory.getLog(GpuOffLineDataProvider.class);
     private static final int CHANNELS = 3, POSTSTIMULUS = 750, FEATURES = 48;
     private final long ctx, odp;
 
-    public GpuOffLineDataProvider(String[] args) {                 // OffLineDataProvider.java:78
+    public GpuOffLineDataProvider(String[] args) throws Exception { // OffLineDataProvider.java:78
+        super(args);
         ctx = nativeCtxCreate(0);                                  // eegfx_ctx_create
         if (ctx == 0) throw new IllegalStateException(nativeLastError());
         odp = nativeOdpCreate(ctx, args);                          // eegfx_odp_create
@@ -28,10 +33,12 @@ public class GpuOffLineDataProvider {
     }
 
     /** :88-98 -- a failure is logged and swallowed; the epochs loaded before it stay. */
+    @Override
     public void loadData() {
         if (nativeOdpLoadData(odp) != 0) logger.fatal(nativeOdpError(odp));
     }
 
+    @Override
     public List<double[][]> getData() {                            // :370-372
         int n = (int) nativeOdpNumEpochs(odp);
         double[] flat = new double[n * CHANNELS * POSTSTIMULUS];
@@ -46,6 +53,7 @@ public class GpuOffLineDataProvider {
         return epochs;
     }
 
+    @Override
     public List<Double> getDataLabels() {                          // :377-379
         int n = (int) nativeOdpNumEpochs(odp);
         double[] lab = new double[n];

@@ -31,16 +31,23 @@ public class GpuWaveletTransform implements IFeatureExtraction {
         }
     };
 
-    private int name, epochSize, skipSamples, featureSize;
+    // WaveletTransform's constructors (WaveletTransform.java:78-98): the defaults are 8, 512, 175
+    // and 16; the four-argument form assigns without the setters' checks, as the reference's
+    // does (an unsupported combination is refused by extractFeatures, EEGFX_ENOTSUP); the one-
+    // argument form goes through setWaveletName.
+    private int epochSize = 512, skipSamples = 175, featureSize = 16;
+    private int name;
 
-    public GpuWaveletTransform() { this(8, 512, 175, 16); }
+    public GpuWaveletTransform() { this.name = 8; }
 
     public GpuWaveletTransform(int name, int epochSize, int skipSamples, int featureSize) {
-        setWaveletName(name);
-        setEpochSize(epochSize);
-        setSkipSamples(skipSamples);
-        setFeatureSize(featureSize);
+        this.name = name;
+        this.epochSize = epochSize;
+        this.skipSamples = skipSamples;
+        this.featureSize = featureSize;
     }
+
+    public GpuWaveletTransform(int name) { setWaveletName(name); }
 
     @Override
     public double[] extractFeatures(double[][] epoch) {
@@ -86,6 +93,34 @@ public class GpuWaveletTransform implements IFeatureExtraction {
     public void setFeatureSize(int featureSize) {
         if (featureSize > 0 && featureSize <= 1024) this.featureSize = featureSize;
         else throw new IllegalArgumentException("Feature Size must be > 0 and <= 1024");
+    }
+
+    // WaveletTransform.java:214-244: same text, same fields compared, same hash
+    @Override
+    public String toString() {
+        return "DWT: EPOCH_SIZE: " + this.epochSize +
+                " FEATURE_SIZE: " + this.featureSize +
+                " WAVELETNAME: " + this.name +
+                " SKIP_SAMPLES: " + this.skipSamples +
+                "\n";
+    }
+
+    @Override
+    public boolean equals(Object o) {
+        if (this == o) return true;
+        if (o == null || getClass() != o.getClass()) return false;
+        GpuWaveletTransform that = (GpuWaveletTransform) o;
+        return epochSize == that.epochSize && skipSamples == that.skipSamples
+                && name == that.name && featureSize == that.featureSize;
+    }
+
+    @Override
+    public int hashCode() {
+        int result = epochSize;
+        result = 31 * result + skipSamples;
+        result = 31 * result + name;
+        result = 31 * result + featureSize;
+        return result;
     }
 
     private static native long nativeCreate(int device);

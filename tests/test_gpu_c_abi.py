@@ -55,3 +55,27 @@ def test_java_shim_sequence_gpu(tmp_path, golden_vectors):
     wm_ref, _ = mllib_logreg.sgd_train(want, labels, 20, 1.0, 0.0, mini_batch_fraction=0.5,
                                        num_partitions=4)
     assert np.linalg.norm(wm - wm_ref) <= 1e-9 * np.linalg.norm(wm_ref)
+
+
+def test_jni_natives_gpu(tmp_path, golden_vectors):
+    """integration/jni/eegfx_jni.c itself, compiled against the mock JNI environment
+    (tests/c_abi/jni_mock/jni.h) and driven as the Java classes drive it
+    (tests/c_abi/jni_consumer.c): provider -> getData / getDataLabels / getFeatures, per-epoch
+    extractFeatures launched and through the resident server, the batch, train / predict /
+    statistics.  Rows equal golden_vectors.json's hex rows; weights the MLlib restatement's."""
+    from oracle import mllib_logreg
+    from test_jni_bindings import _build_jni_consumer
+    exe = _build_jni_consumer(tmp_path)
+    r = subprocess.run([exe, INFO_TRAIN, "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "jni_consumer ok (gpu)" in r.stdout
+    lines = r.stdout.splitlines()
+    rows = [[float.fromhex(v) for v in l.split(":")[1].split()] for l in lines
+            if l.startswith("row ")]
+    want = hexrows(golden_vectors["infoTrain"]["features_hex"])
+    assert np.array_equal(np.array(rows), want)
+    w = np.array([float.fromhex(v) for v in
+                  next(l for l in lines if l.startswith("weights:")).split(":")[1].split()])
+    labels = np.array(golden_vectors["infoTrain"]["labels"], dtype=np.float64)
+    w_ref, _ = mllib_logreg.sgd_train(want, labels, 100, 1.0, 0.01)
+    assert np.linalg.norm(w - w_ref) <= 1e-9 * np.linalg.norm(w_ref)

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -93,8 +94,47 @@ int main() {
   const bool one_launch = false;
   auto fstep = [&] {};
 #endif
+  // PROBE_OVERLAP=K: the step in K chunks, baseline chunks on one stream and window chunks on
+  // another (chunk i's window waits for its baseline; chunk i's baseline of the next step waits
+  // for chunk i's window of this one, whose scratch it reuses), so baselines run under windows
+  const char* ov = getenv("PROBE_OVERLAP");
+  const int K = ov ? atoi(ov) : 0;
+  hipStream_t sb = 0, sw = 0;
+  std::vector<hipEvent_t> evb(K > 0 ? K : 1), evw(K > 0 ? K : 1);
+  std::vector<int64_t> c0(K + 1, 0);
+  std::vector<uint8_t*> cs(K > 0 ? K : 1);
+  if (K > 0) {
+    (void)hipStreamCreateWithFlags(&sb, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&sw, hipStreamNonBlocking);
+    const char* rp = getenv("PROBE_RAMP");  // first chunk = n / (K * ramp), the rest equal
+    const int ramp = rp ? atoi(rp) : 1;
+    c0[1] = n / ((int64_t)K * ramp);
+    for (int i = 2; i <= K; ++i) c0[i] = c0[1] + (n - c0[1]) * (i - 1) / (K - 1);
+    if (K == 1) c0[1] = n;
+    for (int i = 0; i < K; ++i) {
+      (void)hipEventCreateWithFlags(&evb[i], hipEventDisableTiming);
+      (void)hipEventCreateWithFlags(&evw[i], hipEventDisableTiming);
+      (void)hipMalloc(&cs[i], eegfx::fused_scratch_bytes(c0[i + 1] - c0[i], ct));
+      (void)hipEventRecord(evw[i], sw);
+    }
+    fprintf(stderr, "overlap: %d chunks, first %lld epochs\n", K, (long long)c0[1]);
+  }
+  const bool strict = getenv("PROBE_STRICT") != nullptr;  // no overlap across steps
+  auto ostep = [&] {
+    for (int i = 0; i < K; ++i) {
+      const int64_t a0 = c0[i], m = c0[i + 1] - c0[i];
+      (void)hipStreamWaitEvent(sb, evw[strict && i == 0 ? K - 1 : i], 0);
+      (void)eegfx::launch_fused_baseline(sb, raw, nf, ct, sel, ct, pos + a0, m, cs[i], nullptr, nullptr);
+      (void)hipEventRecord(evb[i], sb);
+      (void)hipStreamWaitEvent(sw, evb[i], 0);
+      (void)eegfx::launch_fused_window(sw, raw, nf, ct, sel, ct, pos + a0, m, fast, cs[i],
+                                       out + a0 * 16 * ct, g);
+      (void)hipEventRecord(evw[i], sw);
+    }
+  };
   auto one = [&] {
-    if (one_launch) fstep();
+    if (K > 0) ostep();
+    else if (one_launch) fstep();
     else if (time_step) { baseline(); window(); }
     else if (time_baseline) baseline();
     else window();
@@ -102,12 +142,20 @@ int main() {
   const char* wu = getenv("PROBE_WARMUP");
   const int warm = wu ? atoi(wu) : 200;
   for (int r = 0; r < warm; ++r) one();
-  (void)hipEventRecord(a);
-  for (int r = 0; r < iters; ++r) one();
-  (void)hipEventRecord(b);
-  (void)hipEventSynchronize(b);
   float ms;
-  (void)hipEventElapsedTime(&ms, a, b);
+  if (K > 0) {  // two streams: wall clock between device-wide drains
+    (void)hipDeviceSynchronize();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < iters; ++r) one();
+    (void)hipDeviceSynchronize();
+    ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  } else {
+    (void)hipEventRecord(a);
+    for (int r = 0; r < iters; ++r) one();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+  }
 #ifdef PROBE_TIMESTAMPS
   {  // one more launch with per-workgroup phase timestamps
     const size_t nwg = (size_t)((n + 7) / 8);
@@ -152,7 +200,8 @@ int main() {
   }
 #endif
   (void)hipMemset(out, 0, n * 16 * ct * 8);
-  if (one_launch) fstep();
+  if (K > 0) { ostep(); (void)hipDeviceSynchronize(); }
+  else if (one_launch) fstep();
   else { baseline(); window(); }
   std::vector<double> h(n * 16 * ct);
   (void)hipMemcpy(h.data(), out, h.size() * 8, hipMemcpyDeviceToHost);
@@ -161,6 +210,6 @@ int main() {
   const hipError_t e = hipGetLastError();
   printf("%s %s %s: %.4f ms per launch (%d launches)  checksum %.17g %.17g  %s\n",
          wide ? "wide c32" : "window c3", fast ? "fma" : "exact",
-         one_launch ? "step-1-launch" : time_step ? "step" : time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
+         K > 0 ? "step-overlap" : one_launch ? "step-1-launch" : time_step ? "step" : time_baseline ? "baseline" : "window", ms / iters, iters, s, q, hipGetErrorString(e));
   return e == hipSuccess ? 0 : 1;
 }
