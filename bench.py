@@ -208,8 +208,74 @@ def whole_path_ceiling(C, numerics, n, step_ms, bpe):
         out["energy_bound"] = {"ms": round(ems, 4),
                                "frac": round(n * bpe / (ems * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                "step_over_bound": round(ems / step_ms, 4),
-                               "step_J": e["step_J_measured"], "cap_W": e["step_W"]}
+                               "step_J": e["step_J_measured"], "cap_W": e["step_W"],
+                               "measured_on": "the box of " + CEILING_FILE + " (this box: "
+                                              "whole_path.energy)"}
     return out
+
+
+class EnergyMeter:
+    """Socket energy of the bench's GPU, read from the SMU's energy accumulator (amdsmi, read-only:
+    no setting changes), and the socket power cap.  Unavailable (no amdsmi, no permission, device
+    not matched by PCI address) -> ok False and `why` says so; the bench line then carries null."""
+
+    def __init__(self, torch, dev_index):
+        self.h, self.why, self.smi = None, None, None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self.smi = amdsmi
+            p = torch.cuda.get_device_properties(dev_index)
+            want = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+            for h in amdsmi.amdsmi_get_processor_handles():
+                dom, bus, devfn = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
+                if (int(dom, 16), int(bus, 16), int(devfn.split(".")[0], 16)) == want:
+                    self.h = h
+                    break
+            if self.h is None:
+                self.why = f"no amdsmi device at PCI {want}"
+            else:
+                self.joules()
+        except Exception as e:  # reported, never fatal
+            self.h, self.why = None, repr(e)[:200]
+
+    @property
+    def ok(self):
+        return self.h is not None
+
+    def joules(self):
+        e = self.smi.amdsmi_get_energy_count(self.h)
+        return e["energy_accumulator"] * e["counter_resolution"] * 1e-6
+
+    def cap_w(self):
+        c = self.smi.amdsmi_get_power_cap_info(self.h)["power_cap"]
+        return c / 1e6 if c > 1e5 else float(c)  # microwatts on this stack
+
+
+def energy_leg(meter, torch, dev, step, step_ms, n, bpe, min_ms=300.0):
+    """The live energy bound of the step: untimed steps after the timed region,
+    for at least min_ms, bracketed by the socket's energy accumulator.  A step cannot be shorter
+    than its energy over the socket power cap, so bound_ms = step_J / cap_W, and step_over_bound =
+    bound_ms / step_ms (the timed step) = the power drawn as a fraction of the cap: near 1 means the
+    step is energy-bound at the cap on this box, and only less energy per epoch makes it faster."""
+    if meter is None or not meter.ok:
+        return {"available": False, "why": getattr(meter, "why", "not measured")}
+    k = max(10, int(min_ms / max(step_ms, 1e-3)))
+    torch.cuda.synchronize(dev)
+    j0, t0 = meter.joules(), time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize(dev)
+    j1, t1 = meter.joules(), time.perf_counter()
+    cap = meter.cap_w()
+    e = (j1 - j0) / k
+    bound_ms = e / cap * 1e3
+    return {"available": True, "steps": k, "step_J": round(e, 5),
+            "mean_W": round((j1 - j0) / (t1 - t0), 1), "cap_W": round(cap, 1),
+            "bound_ms": round(bound_ms, 4),
+            "frac_at_bound": round(n * bpe / (bound_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_over_bound": round(bound_ms / step_ms, 4),
+            "source": "amdsmi energy accumulator over the untimed steps after the timed region"}
 
 
 _JSON_OUT = None
@@ -285,6 +351,7 @@ def main():
         raise SystemExit("--spacing must be >= 100 frames")
     n_frames = sp * n + 2000
     ctx = fx.Context(dev.index, numerics=args.numerics)
+    meter = EnergyMeter(torch, dev.index)
     # A dedicated (non-null) torch stream shared with the context: the kernels run on it, so the
     # HIP events recorded on it bracket exactly the launches of the timed region.
     stream = torch.cuda.Stream(dev)
@@ -358,6 +425,7 @@ def main():
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
+    energy = energy_leg(meter, torch, dev, step, step_ms, n, bytes_per_epoch(ct, C))
 
     # the other numerics mode, same buffers (reported beside the headline, not as value)
     alt = None
@@ -441,6 +509,7 @@ def main():
                 "whole_path": {"ms": round(step_ms, 4), "bytes_per_epoch": bpe,
                                "GBps": round(path_gbs, 1),
                                "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                               "energy": energy,
                                "ceiling": whole_path_ceiling(C, args.numerics, n, step_ms, bpe)},
                 # the other side of the kernel's balance: fp64 filter-bank flops
                 # (5,120 MAC per signal) against the vector fp64 peak, and the VALU issue share

@@ -89,6 +89,7 @@ SIGNATURES = {
                                        POINTER(c_int64)]),
     "eegfx_ctx_set_timing": (c_int, [c_void_p, c_int]),
     "eegfx_ctx_set_mailbox": (c_int, [c_void_p, c_int]),
+    "eegfx_ctx_get_mailbox": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "eegfx_ctx_destroy": (c_int, [c_void_p]),
     "eegfx_read_header": (c_int, [c_char_p, POINTER(HeaderInfo), POINTER(ChannelInfo), c_int32]),
     "eegfx_read_markers": (c_int, [c_char_p, POINTER(Marker), c_int64, POINTER(c_int64)]),

@@ -155,6 +155,14 @@ class Context:
         synchronisation (torch.cuda.synchronize), which would wait for the resident kernel."""
         check(lib().eegfx_ctx_set_mailbox(self.handle, 1 if enable else 0))
 
+    def mailbox_state(self):
+        """(enabled, resident) of the context's per-epoch server (eegfx_ctx_get_mailbox): at most
+        4 contexts of a process hold a started server on a device; the others use the launch
+        path."""
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().eegfx_ctx_get_mailbox(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return bool(a.value), bool(b.value)
+
     def guard_detail(self, reset: bool = False):
         """(rows checked, rows that went to the guard's second stage, rows recomputed under EXACT)
         since the context was created or last reset (eegfx_ctx_guard_detail; synchronises)."""

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -223,39 +224,55 @@ struct eegfx_ctx {
   }
   // The opt-in resident small-batch server (eegfx_ctx_set_mailbox, features_mailbox_kernel): a
   // host-mapped command block, the kernel's own stream (never the context stream: the kernel
-  // stays resident), the request sequence and the time of the last request.
-  bool mailbox = false;
+  // stays resident), the request sequence and the time of the last request.  A server needs a
+  // hardware queue of its own (a queue runs its packets in order: a second kernel behind a
+  // resident one waits for it to idle out), and the highest-priority pool has kMbSlotsPerDevice of
+  // them, so at most that many contexts of the process hold a server slot on a device
+  // (mb_acquire); the others serve their calls on the launch path, and take a slot when one frees.
+  bool mailbox = false;   // enabled by the caller
+  bool mb_slot = false;   // holds one of the device's server slots
   hipStream_t mb_stream = nullptr;
   MailboxCmd* mb_host = nullptr;
   MailboxCmd* mb_dev = nullptr;
   uint32_t mb_seq = 0;
-  bool mb_live = false;  // launched and not stopped by the host (it may still have idled out)
+  uint32_t mb_gen = 0;      // launch generation (MailboxCmd::alive)
+  bool mb_live = false;     // launched and not stopped by the host (it may still have idled out)
+  bool mb_started = false;  // the live server has published its generation
+  bool mb_stuck = false;    // a server that did not start in time: stopped, not yet returned
   std::chrono::steady_clock::time_point mb_last{};
   static constexpr uint64_t kMbIdleTicks = 100000000;  // 1 s of s_memrealtime (100 MHz)
   void mb_launch() {
     // the staging a server reads is fixed for its lifetime (growing it stops the server first)
     mb_host->rows = pin_in.p ? (const double*)pin_in.device_ptr() : nullptr;
     mb_host->out = pin_out.p ? (double*)pin_out.device_ptr() : nullptr;
-    HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks));
+    if (++mb_gen == 0) mb_gen = 1;
+    HIP_CHECK(launch_features_mailbox(mb_stream, mb_dev, kMbIdleTicks, mb_gen));
     mb_live = true;
+    mb_started = false;
   }
-  void mb_stop() {
-    if (!mb_host) return;
+  // Stops a live server: `stop` is seen within one poll.  A server that has not returned after
+  // 10 s (100 ms if it has not been seen to start: its queue is held by another resident kernel)
+  // keeps `stop` set, so it returns as soon as it runs, and is marked stuck; mb_ready clears
+  // `stop` once it has returned.
+  // Returns whether the kernel has returned.
+  bool mb_stop() {
+    if (!mb_host || !mb_live) return true;
     __atomic_store_n(&mb_host->stop, 1u, __ATOMIC_RELEASE);
-    // the kernel sees `stop` within one poll; a server that does not return is reported, not
-    // waited on forever
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t q;
     while ((q = hipStreamQuery(mb_stream)) == hipErrorNotReady) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      if (std::chrono::steady_clock::now() - t0 >
+          (mb_started ? std::chrono::milliseconds(10000) : std::chrono::milliseconds(100))) {
         mb_live = false;
-        fail(EEGFX_EHIP, "mailbox server did not stop within 10 s");
+        mb_stuck = true;
+        return false;
       }
       std::this_thread::yield();
     }
     __atomic_store_n(&mb_host->stop, 0u, __ATOMIC_RELEASE);
     mb_live = false;
     HIP_CHECK(q);
+    return true;
   }
   // hipSuccess: the server kernel has returned; hipErrorNotReady: it is running; anything else
   // is an error of the stream and is raised
@@ -265,20 +282,25 @@ struct eegfx_ctx {
     HIP_CHECK(q);
     return true;
   }
-  // One request: n epochs of packed window rows in pin_in -> rows in pin_out.
+  // Whether the resident server takes this call (false: the launch path).  Takes a device slot
+  // and sets the server up on first use; restarts a server that may be near its 1 s idle exit
+  // (no request for 500 ms) so a request never races that exit; posts nothing until the server
+  // has published its generation, and falls back to the launch path (marking the server stuck)
+  // if it has not started within kMbStartWait.
+  static constexpr auto kMbStartWait = std::chrono::milliseconds(20);
+  bool mb_ready();
+  // One request: n epochs of packed window rows in pin_in -> rows in pin_out (after mb_ready).
   void mb_serve(int64_t n, int C, int nfeat) {
     MailboxCmd* m = mb_host;
     if (++mb_seq == 0) mb_seq = 1;  // 0 means "no request" to the kernel
     const auto now = std::chrono::steady_clock::now();
-    // the kernel returns after 1 s without a request: relaunch it when it may have
-    if (!mb_live || (now - mb_last > std::chrono::milliseconds(500) && mb_returned())) mb_launch();
     __atomic_store_n(&m->req, mailbox_request(mb_seq, C, nfeat, n), __ATOMIC_RELEASE);
     for (uint64_t spin = 1;; ++spin) {
       if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == mb_seq) break;
       if ((spin & 4095) == 0) {
-        // the kernel went idle between the check above and the request: serve it again
-        if (mb_returned() && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != mb_seq)
-          mb_launch();
+        // a server that returned with the request pending (an error, or a stop from another
+        // path): serve it again on the same stream, after that kernel
+        if (mb_returned() && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != mb_seq) mb_launch();
         if (std::chrono::steady_clock::now() - now > std::chrono::seconds(30))
           fail(EEGFX_EHIP, "mailbox request %u not served within 30 s", mb_seq);
       }
@@ -286,15 +308,7 @@ struct eegfx_ctx {
     }
     mb_last = std::chrono::steady_clock::now();
   }
-  void release_mailbox() {
-    if (mb_host) mb_stop();
-    if (mb_stream) (void)hipStreamDestroy(mb_stream);
-    if (mb_host) (void)hipHostFree(mb_host);
-    mb_host = nullptr;
-    mb_dev = nullptr;
-    mb_stream = nullptr;
-    mailbox = false;
-  }
+  void release_mailbox();
   void release_stream_resources() {
     release_mailbox();
     if (small_done) (void)hipEventDestroy(small_done);
@@ -354,6 +368,103 @@ struct eegfx_ctx {
     n_timed = 0;
   }
 };
+
+namespace {
+
+// Resident-server slots per device (eegfx_ctx::mb_ready): the highest-priority hardware queues
+// of the process (4 on the box: a fifth server shares a queue and waits behind another until it
+// idles out).
+constexpr int kMbSlotsPerDevice = 4;
+constexpr int kMbMaxDevices = 64;
+std::mutex g_mb_mu;
+int g_mb_used[kMbMaxDevices] = {};
+bool mb_acquire(int dev) {
+  if (dev < 0 || dev >= kMbMaxDevices) return false;
+  std::lock_guard<std::mutex> l(g_mb_mu);
+  if (g_mb_used[dev] >= kMbSlotsPerDevice) return false;
+  ++g_mb_used[dev];
+  return true;
+}
+void mb_release(int dev) {
+  std::lock_guard<std::mutex> l(g_mb_mu);
+  if (dev >= 0 && dev < kMbMaxDevices && g_mb_used[dev] > 0) --g_mb_used[dev];
+}
+
+}  // namespace
+
+bool eegfx_ctx::mb_ready() {
+  if (!mailbox) return false;
+  if (mb_stuck) {  // a server that never started: the launch path until it has run and returned
+    if (!mb_returned()) return false;
+    __atomic_store_n(&mb_host->stop, 0u, __ATOMIC_RELEASE);
+    mb_stuck = false;
+  }
+  if (!mb_slot) {
+    if (!mb_acquire(device)) return false;
+    mb_slot = true;
+  }
+  if (!mb_stream) {
+    try {
+      // A stream of the highest priority: the runtime multiplexes a process's streams of one
+      // priority over a few hardware queues, and a queue runs its packets in order, so a
+      // normal-priority stream sharing the resident kernel's queue would wait behind it (up to
+      // its 1 s idle exit).  The high-priority pool keeps the server on a queue of its own while
+      // no more than kMbSlotsPerDevice servers exist.
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_CHECK(hipStreamCreateWithPriority(&mb_stream, hipStreamNonBlocking, greatest));
+      HIP_CHECK(hipHostMalloc((void**)&mb_host, sizeof(MailboxCmd),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+      memset(mb_host, 0, sizeof(MailboxCmd));
+      HIP_CHECK(hipHostGetDevicePointer((void**)&mb_dev, mb_host, 0));
+      mb_seq = 0;
+    } catch (...) {
+      release_mailbox();
+      mailbox = true;  // still enabled: later calls retry
+      throw;
+    }
+  }
+  const auto now = std::chrono::steady_clock::now();
+  // no request for 500 ms: the server may be close to its 1 s idle exit -- restart it, so no
+  // request is ever posted to a kernel that is returning
+  if (mb_live && now - mb_last > std::chrono::milliseconds(500)) {
+    if (!mb_stop()) return false;
+  }
+  if (!mb_live) {
+    mb_launch();
+    mb_last = now;
+  }
+  if (!mb_started) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&mb_host->alive, __ATOMIC_ACQUIRE) != mb_gen) {
+      if (std::chrono::steady_clock::now() - t0 > kMbStartWait) {
+        // still queued: it returns at once when it runs (stop), the call takes the launch path
+        __atomic_store_n(&mb_host->stop, 1u, __ATOMIC_RELEASE);
+        mb_live = false;
+        mb_stuck = true;
+        return false;
+      }
+      __builtin_ia32_pause();
+    }
+    mb_started = true;
+  }
+  return true;
+}
+
+void eegfx_ctx::release_mailbox() {
+  const bool stopped = mb_stop();
+  if (mb_stream && stopped && !mb_stuck) (void)hipStreamDestroy(mb_stream);
+  if (mb_host && stopped && !mb_stuck) (void)hipHostFree(mb_host);
+  // a stuck server keeps its stream and command block (it still reads `stop` when it runs):
+  // leaked rather than freed under a queued kernel
+  mb_host = nullptr;
+  mb_dev = nullptr;
+  mb_stream = nullptr;
+  mb_live = mb_started = mb_stuck = false;
+  if (mb_slot) mb_release(device);
+  mb_slot = false;
+  mailbox = false;
+}
 
 namespace {
 
@@ -780,26 +891,16 @@ int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable) {
       return;
     }
     if (ctx->mailbox) return;
-    ctx->mailbox = true;  // from here on release_mailbox undoes whatever was set up
-    try {
-      // A stream of the highest priority: the runtime multiplexes a process's streams of one
-      // priority over a few hardware queues (4 here), and a queue runs its packets in order, so
-      // a normal-priority stream sharing the resident kernel's queue would wait behind it (up to
-      // its 1 s idle exit).  The high-priority pool keeps the server on a queue of its own.
-      int least = 0, greatest = 0;
-      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      HIP_CHECK(hipStreamCreateWithPriority(&ctx->mb_stream, hipStreamNonBlocking, greatest));
-      HIP_CHECK(hipHostMalloc((void**)&ctx->mb_host, sizeof(MailboxCmd),
-                              hipHostMallocMapped | hipHostMallocCoherent));
-      memset(ctx->mb_host, 0, sizeof(MailboxCmd));
-      HIP_CHECK(hipHostGetDevicePointer((void**)&ctx->mb_dev, ctx->mb_host, 0));
-      ctx->mb_seq = 0;
-      ctx->mb_launch();
-      ctx->mb_last = std::chrono::steady_clock::now();
-    } catch (...) {
-      ctx->release_mailbox();
-      throw;
-    }
+    ctx->mailbox = true;  // the server starts on the first one-epoch call that gets a slot
+    (void)ctx->mb_ready();
+  });
+}
+
+int eegfx_ctx_get_mailbox(eegfx_ctx* ctx, int32_t* enabled, int32_t* resident) {
+  return guarded([&] {
+    if (!ctx) fail(EEGFX_EINVAL, "null context");
+    if (enabled) *enabled = ctx->mailbox ? 1 : 0;
+    if (resident) *resident = ctx->mailbox && ctx->mb_slot && ctx->mb_live && ctx->mb_started ? 1 : 0;
   });
 }
 
@@ -958,7 +1059,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         // under both numerics (kernels.hip small_epoch), so the fma guard does not count them.
         // growing a pinned buffer frees the old one, which synchronises the device: stop the
         // resident server first (the next request restarts it)
-        if (ctx->mailbox && ((size_t)n * C * row_w > ctx->pin_in.cap || out_bytes > ctx->pin_out.cap))
+        if (ctx->mb_live && ((size_t)n * C * row_w > ctx->pin_in.cap || out_bytes > ctx->pin_out.cap))
           ctx->mb_stop();
         double* hin = (double*)ctx->pin_in.get((size_t)n * C * row_w);
         double* hout = (double*)ctx->pin_out.get(out_bytes);
@@ -967,8 +1068,9 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         // The resident server (no launch, no stream sync) takes single epochs: it serves a
         // request's epochs one after another (~7 us each), where a launch runs them on a
         // workgroup each (11 epochs: ~20 us launched against ~80 us served).
-        if (ctx->mailbox && n == 1) {
+        if (n == 1 && ctx->mb_ready()) {
           ctx->mb_serve(n, C, feature_size);
+          ctx->check_positions_flag();  // as every synchronising call (the launch path below)
           memcpy(out, hout, out_bytes);
           return;
         }
@@ -1156,7 +1258,7 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
     };
     try {
       if (!pinned) {  // the context's grow-only staging (a growth frees: stop our server first)
-        if (ctx->mailbox && cbytes > std::min(ctx->pin_chunk[0].cap, ctx->pin_chunk[1].cap))
+        if (ctx->mb_live && cbytes > std::min(ctx->pin_chunk[0].cap, ctx->pin_chunk[1].cap))
           ctx->mb_stop();
         for (int b = 0; b < 2; ++b) pin[b] = ctx->pin_chunk[b].get(cbytes);
       }

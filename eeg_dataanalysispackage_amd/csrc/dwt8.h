@@ -419,13 +419,69 @@ static __constant__ double kH5[kH5Size] = EEGFX_H5_TABLE;
 
 // The core takes the samples through two callables: fetch(k) reads raw sample k of the lane's
 // slice (k < 64) and decode(v0, v1, x0, x1) turns the raw pair (k, k + 32) into doubles.
+// EEGFX_LDS_B64 (A/B builds): the int16 kernels read samples k and k + 1 of a signal with one
+// 8-byte LDS read (dwt8_collapsed_core_b64) instead of two 2-byte reads.
+#ifndef EEGFX_LDS_B64
+#define EEGFX_LDS_B64 0
+#endif
+typedef const __attribute__((address_space(4))) double* dwt8_const_f64_ptr;
+
+// The four-point update of pair n (x0 = sample n, x1 = sample n + 32) into the 12 accumulators.
+__device__ __forceinline__ void toom_pair(dwt8_const_f64_ptr tab, int n, double x0, double x1,
+                                          double (&A0)[3], double (&Ai)[3], double (&Bp)[3],
+                                          double (&Bm)[3]) {
+  // exact when the pair's exponents lie within 29 of each other (the decoded fp32 samples of a
+  // window nearly always do); otherwise, and for caller-supplied doubles
+  // (features_from_epochs_kernel), one rounding each -- tools/fma_bound.py models both adds as
+  // rounded, so the guard's bound covers either case
+  const double xp = x1 + x0, xm = x1 - x0;
+  const dwt8_const_f64_ptr R = tab + n * kH5Cols;  // this pair's 12 constants (96 bytes)
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
+    if (n + 32 * (3 * q + 2) < 280)
+      Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
+    Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
+    Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
+  }
+  // The pair's updates complete here: without this, the IR ends up ordered chain by chain (all
+  // 64 sample reads and 32 constant rows first, every multiply-add after them), which spills.
+  asm volatile("" : "+v"(A0[0]), "+v"(A0[1]), "+v"(A0[2]), "+v"(Ai[0]), "+v"(Ai[1]), "+v"(Ai[2]),
+               "+v"(Bp[0]), "+v"(Bp[1]), "+v"(Bp[2]), "+v"(Bm[0]), "+v"(Bm[1]), "+v"(Bm[2]));
+}
+
+// Interpolation of the four-point accumulators into the ten partial sums, the one partial-sum
+// round that completes a5[2s], a5[2s+1], and level 6.
+__device__ __forceinline__ void toom_finish(const double (&A0)[3], const double (&Ai)[3],
+                                            const double (&Bp)[3], const double (&Bm)[3],
+                                            int gbase, int s, double& a6, double& d6) {
+  double P[10];  // P[j + 1]
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    P[3 * q] = q > 0 ? A0[q] + Ai[q - 1] : A0[q];
+    P[3 * q + 1] = Bp[q] - Bm[q] - Ai[q];
+    P[3 * q + 2] = Bp[q] + Bm[q] - A0[q];
+  }
+  P[9] = Ai[2];
+  double a5[2 + 8];
+  a5[0] = P[1];
+  a5[1] = P[0];
+#pragma unroll
+  for (int d = 1; d <= 4; ++d) {
+    const int src = gbase + ((s + d) & (kLanesPerSignal - 1));
+    a5[0] += __shfl(P[2 * d + 1], src, 64);
+    a5[1] += __shfl(P[2 * d], src, 64);
+  }
+  halo<2, true>(a5, nullptr, gbase, s);
+  a6 = fir10<true, false>(a5);
+  d6 = fir10<true, true>(a5);
+}
+
 template <typename Fetch, typename Decode>
 __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, int gbase, int s,
                                                     double& a6, double& d6) {
-  typedef const __attribute__((address_space(4))) double* const_f64_ptr;
-  const_f64_ptr tab = (const_f64_ptr)kH5;
+  dwt8_const_f64_ptr tab = (dwt8_const_f64_ptr)kH5;
   asm volatile("" : "+s"(tab));  // scalar loads of the table, not per-tap literal moves
-  double P[10];  // P[j + 1]
 #if EEGFX_TOOM
   double A0[3], Ai[3], Bp[3], Bm[3];
   // the samples are fetched two pairs ahead of their use (the per-pair ordering below otherwise
@@ -440,33 +496,11 @@ __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, 
     if (n + 2 < 32) { vq[n % 2][0] = fetch(n + 2); vq[n % 2][1] = fetch(n + 2 + 32); }
     double x0, x1;
     decode(v0, v1, x0, x1);
-    // exact when the pair's exponents lie within 29 of each other (the decoded fp32 samples of a
-    // window nearly always do); otherwise, and for caller-supplied doubles
-    // (features_from_epochs_kernel), one rounding each -- tools/fma_bound.py models both adds as
-    // rounded, so the guard's bound covers either case
-    const double xp = x1 + x0, xm = x1 - x0;
-    const const_f64_ptr R = tab + n * kH5Cols;  // this pair's 12 constants (96 bytes)
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
-      if (n + 32 * (3 * q + 2) < 280)
-        Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
-      Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
-      Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
-    }
-    // The pair's updates complete here: without this, the IR ends up ordered chain by chain (all
-    // 64 sample reads and 32 constant rows first, every multiply-add after them), which spills.
-    asm volatile("" : "+v"(A0[0]), "+v"(A0[1]), "+v"(A0[2]), "+v"(Ai[0]), "+v"(Ai[1]), "+v"(Ai[2]),
-                 "+v"(Bp[0]), "+v"(Bp[1]), "+v"(Bp[2]), "+v"(Bm[0]), "+v"(Bm[1]), "+v"(Bm[2]));
+    toom_pair(tab, n, x0, x1, A0, Ai, Bp, Bm);
   }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    P[3 * q] = q > 0 ? A0[q] + Ai[q - 1] : A0[q];
-    P[3 * q + 1] = Bp[q] - Bm[q] - Ai[q];
-    P[3 * q + 2] = Bp[q] + Bm[q] - A0[q];
-  }
-  P[9] = Ai[2];
+  toom_finish(A0, Ai, Bp, Bm, gbase, s, a6, d6);
 #else
+  double P[10];  // P[j + 1]
   // the direct form (A/B builds only): 18 multiply-adds per pair, one scheduling region per pair
   // (without it the c3 kernel hoisted tap rows into SGPRs and spilled them to VGPR lanes)
 #pragma unroll
@@ -483,7 +517,6 @@ __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-#endif
   double a5[2 + 8];
   a5[0] = P[1];
   a5[1] = P[0];
@@ -496,6 +529,34 @@ __device__ __forceinline__ void dwt8_collapsed_core(Fetch fetch, Decode decode, 
   halo<2, true>(a5, nullptr, gbase, s);
   a6 = fir10<true, false>(a5);
   d6 = fir10<true, true>(a5);
+#endif
+}
+
+// The same core for int16 samples in a 3-channel multiplexed window: fetch2(k) reads the 8 bytes
+// from sample k of the lane's signal, whose int16 words 0 and 3 are samples k and k + 1 (a frame
+// is 3 words), so one LDS read serves two pairs.  Group g = pairs 2g and 2g + 1; the next group's
+// two reads are issued before the current group's updates.
+template <typename Fetch2, typename Decode>
+__device__ __forceinline__ void dwt8_collapsed_core_b64(Fetch2 fetch2, Decode decode, int gbase,
+                                                        int s, double& a6, double& d6) {
+  dwt8_const_f64_ptr tab = (dwt8_const_f64_ptr)kH5;
+  asm volatile("" : "+s"(tab));
+  double A0[3], Ai[3], Bp[3], Bm[3];
+  uint64_t q0 = fetch2(0), q1 = fetch2(32);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const uint64_t c0 = q0, c1 = q1;
+    if (g + 1 < 16) { q0 = fetch2(2 * g + 2); q1 = fetch2(2 * g + 34); }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int v0 = h == 0 ? (int)(int16_t)(uint16_t)c0 : (int)(int16_t)(uint16_t)(c0 >> 48);
+      const int v1 = h == 0 ? (int)(int16_t)(uint16_t)c1 : (int)(int16_t)(uint16_t)(c1 >> 48);
+      double x0, x1;
+      decode(v0, v1, x0, x1);
+      toom_pair(tab, 2 * g + h, x0, x1, A0, Ai, Bp, Bm);
+    }
+  }
+  toom_finish(A0, Ai, Bp, Bm, gbase, s, a6, d6);
 }
 
 // The fused kernels' form: raw samples decoded as (double)((float)v * r - b), two correctly
@@ -520,6 +581,23 @@ __device__ __forceinline__ void dwt8_collapsed_cascade(Fetch fetch, float r, flo
       },
       gbase, s, a6, d6);
   if constexpr (TRACK) *ymax = m;
+}
+
+// dwt8_collapsed_cascade over dwt8_collapsed_core_b64 (3-channel int16 windows in LDS).
+template <typename Fetch2>
+__device__ __forceinline__ void dwt8_collapsed_cascade_b64(Fetch2 fetch2, float r, float b,
+                                                           int gbase, int s, double& a6,
+                                                           double& d6) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  dwt8_collapsed_core_b64(
+      fetch2,
+      [&](int v0, int v1, double& x0, double& x1) {
+        const dwt8_f32x2 v = {(float)v0, (float)v1};
+        const dwt8_f32x2 y = v * rr - bb;
+        x0 = (double)y.x;
+        x1 = (double)y.y;
+      },
+      gbase, s, a6, d6);
 }
 
 // The largest value of v over the 8 lanes of a signal group.

@@ -214,7 +214,13 @@ __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* n
                                             float b, int gbase, int s, double& a6, double& d6) {
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
-    dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
+    if constexpr (EEGFX_LDS_B64 && CT == 3) {
+      typedef uint64_t u64_a2 __attribute__((aligned(2)));
+      dwt8_collapsed_cascade_b64([&](int k) { return *(const u64_a2*)(own + k * CT); }, r, b,
+                                 gbase, s, a6, d6);
+    } else {
+      dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
+    }
 #else
     dwt8_fast_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);
 #endif
@@ -328,6 +334,11 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 #ifndef EEGFX_WIN_SUBS
 #define EEGFX_WIN_SUBS 1
 #endif
+// the guard's second stage in the 3-channel window kernel: every flagged row of a sub-tile in one
+// pass (recheck_c3_rows), or (0, A/B builds) one row at a time (recheck_c3)
+#ifndef EEGFX_RECHECK_ROWS
+#define EEGFX_RECHECK_ROWS 1
+#endif
 template <int CT, int C, bool FAST, bool NT, int SUBS = EEGFX_WIN_SUBS>
 __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
@@ -408,13 +419,26 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
           },
           C, 16, fb + kSub * F, row, lane);
     };
-    // the guard's second stage: the row's measured max |x| per channel (recheck_c3), from the
-    // staged window (epochs 1-7; epoch 0's window lies under the rows: from the recording)
+    // the guard's second stage: the rows' measured max |x|, from the staged windows (epochs
+    // 1-7, recheck_c3_rows: every flagged row of the sub-tile in one pass; epoch 0's window lies
+    // under the rows: from the recording, recheck_c3)
+#if EEGFX_RECHECK_ROWS
+    auto recheck = [&](uint64_t flagged, double acc) {
+      return recheck_c3_rows<G::SEGQ, G::ESTR * 4>(
+          flagged, acc, sel, base + e0 * C, (const uint8_t*)win, delta, lane, [&] {
+            return recheck_c3<G::FB, G::SEGQ>(raw, n_frames, sel, wb[e0], base + e0 * C,
+                                              nullptr, true, lane);
+          });
+    };
+    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo, recheck);
+#else
     auto recheck = [&](int e) {
       return recheck_c3<G::FB, G::SEGQ>(raw, n_frames, sel, wb[e0 + e], base + (e0 + e) * C,
                             (const uint8_t*)(win + e * G::ESTR), e == 0, lane);
     };
-    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo, recheck);
+    normalise_store<F, FAST, C>(fb, norm, out + e0 * F, ne, lane, gx, guard, redo,
+                                per_row_recheck(recheck));
+#endif
   }
 }
 

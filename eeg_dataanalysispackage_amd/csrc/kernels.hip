@@ -411,7 +411,8 @@ __global__ __launch_bounds__(256) void cut_features_c3_kernel(
       return recheck_c3<FB, 1>((const uint8_t*)raw, n_frames, sel, (sP[e] + 175) * FB,
                             s_base + e * C, nullptr, true, lane);
     };
-    normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo, recheck);
+    normalise_store<F, FAST, C>(fb, norm, fout + e0 * F, ne, lane, gx, guard, redo,
+                                per_row_recheck(recheck));
   }
 }
 
@@ -848,8 +849,12 @@ __global__ __launch_bounds__(256) void features_small_kernel(const double* __res
 // features_small_kernel does, and written to its pinned output, then the completed sequence
 // number is published (system-scope release after every wave's stores).  The kernel returns when
 // the host sets `stop`, or after idle_ticks (s_memrealtime, 100 MHz) without a request -- every
-// wave reaches that exit; the host relaunches it on the next request.
-__global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, uint64_t idle_ticks) {
+// wave reaches that exit; the host relaunches it on the next request.  At entry it publishes its
+// launch generation in `alive`: the host posts a request only to a server that has started (a
+// kernel still queued behind other work is never handed a request the launch path might also
+// serve).
+__global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, uint64_t idle_ticks,
+                                                               uint32_t gen) {
   __shared__ __attribute__((aligned(16))) SmallLds sh;
   __shared__ uint32_t cmd[2];  // request to serve, 0 = return
   const int tid = threadIdx.x;
@@ -863,6 +868,7 @@ __global__ __launch_bounds__(256) void features_mailbox_kernel(MailboxCmd* mb, u
       (int)__hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
   const double* rows = mb->rows;
   double* out = mb->out;
+  if (tid == 0) __hip_atomic_store(&mb->alive, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
     if (wave0) {
       uint64_t go = 0;
@@ -1111,8 +1117,9 @@ hipError_t launch_features_from_epochs(hipStream_t st, const double* ep, int64_t
 
 bool features_small_supported(int C) { return C >= 1 && C <= dev::kSmallMaxC; }
 
-hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks) {
-  hipLaunchKernelGGL(dev::features_mailbox_kernel, dim3(1), dim3(256), 0, st, mb, idle_ticks);
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
+                                   uint32_t gen) {
+  hipLaunchKernelGGL(dev::features_mailbox_kernel, dim3(1), dim3(256), 0, st, mb, idle_ticks, gen);
   return hipGetLastError();
 }
 

@@ -55,6 +55,8 @@ struct MailboxCmd {
   uint64_t req;
   uint32_t done;  // the last sequence number whose rows are in `out` (device)
   uint32_t stop;  // 1: the kernel returns
+  uint32_t alive;  // the launch generation of the kernel that has started (device, at entry)
+  uint32_t pad_;
   // staging, fixed while a server runs (growing it stops the server first); read at kernel start
   const double* rows;  // device-mapped pinned [n][C][512] window doubles
   double* out;         // device-mapped pinned [n][C * nfeat] rows
@@ -63,7 +65,8 @@ inline uint64_t mailbox_request(uint32_t seq, int C, int nfeat, int64_t n) {
   return (uint64_t)seq << 32 | (uint64_t)(C - 1) << 26 | (uint64_t)(nfeat - 1) << 21 |
          (uint64_t)n;
 }
-hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks);
+hipError_t launch_features_mailbox(hipStream_t st, MailboxCmd* mb, uint64_t idle_ticks,
+                                   uint32_t gen);
 hipError_t launch_features_small(hipStream_t st, const double* rows, int64_t n, int C, int nfeat,
                                  double* out);
 hipError_t launch_synth(hipStream_t st, int16_t* dst, int64_t n_frames, int ct, uint64_t seed);

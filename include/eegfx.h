@@ -133,8 +133,16 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
  * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
  * (hipDeviceSynchronize, hipFree, hipHostFree) waits for it: disable it before such calls.  Its
  * stream has the highest priority, which keeps it on a hardware queue of its own (streams of one
- * priority share a few queues in order).  Off by default. */
+ * priority share a few queues in order).  That pool has 4 queues, so at most 4
+ * contexts of a process hold a server on one device at a time: a context enabled beyond that
+ * serves its calls on the launch path (same rows) and takes a server once a slot frees.  A
+ * server that has not started within 20 ms of its launch (its queue held by other work) is
+ * stopped and the call takes the launch path; no request is ever posted to a server that has not
+ * started.  Off by default. */
 int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable);
+/* Whether the resident server is enabled on ctx and whether it currently holds a slot with a
+ * started server (either pointer may be NULL). */
+int eegfx_ctx_get_mailbox(eegfx_ctx* ctx, int32_t* enabled, int32_t* resident);
 int eegfx_ctx_destroy(eegfx_ctx* ctx);
 
 /* ---- BrainVision reader (replaces eegloader-hdfs 2.4 cz.zcu.kiv.signal.*, pom.xml:84-88) - */

@@ -110,3 +110,39 @@ def test_gather_row_checksum_detects_misplaced_shards():
     rows = shards[2].clone()
     rows[[3, 4]] = rows[[4, 3]]                       # two rows exchanged inside a shard
     assert bench.row_checksum(rows) != sums[2]
+
+
+def test_live_energy_leg_arithmetic():
+    """whole_path.energy: step energy from the accumulator over the untimed steps, the bound
+    step_J / cap and its ratio to the timed step (a stand-in meter: 1.4 kW drawn, cap 1.4 kW)."""
+    import time as _time
+
+    class FakeTorch:
+        class cuda:
+            @staticmethod
+            def synchronize(dev):
+                pass
+
+    class Meter:
+        ok = True
+        j = 0.0
+
+        def joules(self):
+            return self.j
+
+        def cap_w(self):
+            return 1400.0
+
+    m = Meter()
+
+    def step():   # each step: 0.88 ms of wall time at 1.4 kW
+        m.j += 1400.0 * 0.88e-3
+        _time.sleep(0.0)
+
+    e = bench.energy_leg(m, FakeTorch, None, step, 0.88, 1_000_000, 4064, min_ms=10.0)
+    assert e["available"] and e["steps"] >= 10
+    assert abs(e["step_J"] - 1.232) < 1e-9
+    assert abs(e["bound_ms"] - 0.88) < 1e-4 and abs(e["step_over_bound"] - 1.0) < 1e-3
+    assert abs(e["frac_at_bound"] - 4064e6 / 0.88e-3 / 8e12) < 1e-3
+    off = bench.energy_leg(None, FakeTorch, None, step, 0.88, 1, 4064)
+    assert off["available"] is False

@@ -20,13 +20,13 @@ DMA_ISSUE = """    if (dma_issue<CT, C, NT>(raw, nbytes, wb, e0, ne, win, w, lan
       dma_fixup<CT, C>(raw, nbytes, wb, e0, ne, win, w, lane, rows);"""
 
 FMA_BODY = """#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
-      if (n + 32 * (3 * q + 2) < 280)
-        Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
-      Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
-      Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
-    }"""
+  for (int q = 0; q < 3; ++q) {
+    A0[q] = n == 0 ? x1 * R[q] : __builtin_fma(x1, R[q], A0[q]);
+    if (n + 32 * (3 * q + 2) < 280)
+      Ai[q] = n == 0 ? x0 * R[3 + q] : __builtin_fma(x0, R[3 + q], Ai[q]);
+    Bp[q] = n == 0 ? xp * R[6 + q] : __builtin_fma(xp, R[6 + q], Bp[q]);
+    Bm[q] = n == 0 ? xm * R[9 + q] : __builtin_fma(xm, R[9 + q], Bm[q]);
+  }"""
 
 BASELINE_T32 = [
     ("fused.hip", "  const dim3 g((unsigned)((n + 63) / 64));",
@@ -101,17 +101,17 @@ ABLATIONS = {
         "no LDS sample reads: each sample is an opaque per-lane float plus its index (one fp32 "
         "add in place of the int16 conversion); window DMA, decode and fp64 kept (wrong results)",
         [("fused.hip",
-          "    dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);",
-          "    float q = (float)((int)(uintptr_t)own & 1023);  // ablation: no LDS sample reads\n"
-          "    asm volatile(\"\" : \"+v\"(q));\n"
-          "    dwt8_collapsed_cascade([&](int k) { return q + (float)k; }, r, b, gbase, s, a6, d6);")]),
+          "      dwt8_collapsed_cascade([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6, d6);",
+          "      float q = (float)((int)(uintptr_t)own & 1023);  // ablation: no LDS sample reads\n"
+          "      asm volatile(\"\" : \"+v\"(q));\n"
+          "      dwt8_collapsed_cascade([&](int k) { return q + (float)k; }, r, b, gbase, s, a6, d6);")]),
     "nofp64": (
         "fp64 filter bank removed: the 440 multiply-adds and adds per lane become 64 fp64 adds; "
         "DMA, LDS reads and decode kept (wrong results)",
-        [("dwt8.h", FMA_BODY, """    (void)R;  // ablation: no fp64 filter work, the decoded samples are summed
-    if (n == 0) {
-      for (int q = 0; q < 3; ++q) { A0[q] = x1; Ai[q] = x0; Bp[q] = xp; Bm[q] = xm; }
-    } else { A0[n % 3] += x1; Ai[n % 3] += x0; }""")]),
+        [("dwt8.h", FMA_BODY, """  (void)R;  // ablation: no fp64 filter work, the decoded samples are summed
+  if (n == 0) {
+    for (int q = 0; q < 3; ++q) { A0[q] = x1; Ai[q] = x0; Bp[q] = xp; Bm[q] = xm; }
+  } else { A0[n % 3] += x1; Ai[n % 3] += x0; }""")]),
 }
 
 
