@@ -941,6 +941,12 @@ def bench_stream(args, rank, world, dev, dist):
     torch.cuda.synchronize(dev)
     copy_ms = (time.perf_counter() - c0) / 5 * 1e3
     del d_in, d_out
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0:
+        # the same recordings and marker grid on the host cores (BASELINE.json configs[4])
+        cpu = cpu_baseline(args, torch.from_numpy(raw), torch.from_numpy(out), 3, 3,
+                           sp=step_frames, first=int(pos[0]), n_epochs=n,
+                           what="first streamed 4 h recording (a marker every 100 frames)")
     if rank == 0:
         h2d = nf * 6 * args.steps / el / 1e9
         emit(({
@@ -959,6 +965,7 @@ def bench_stream(args, rank, world, dev, dist):
                           "note": "every frame crosses the host link once per step and every "
                                   "feature row once back; copy_only_ms = the same bytes moved by "
                                   "two concurrent plain copies (the bound), frac = that / step"},
+            "cpu_baseline": cpu,
         }))
     ctx.close()
 
@@ -1076,7 +1083,8 @@ def host_cores():
     return cores, {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_quota_cpus": quota}
 
 
-def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
+def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH, first=None, n_epochs=None,
+                 what="rank-0 synthetic recording"):
     """C restatement of the Java algorithm (oracle/, reference-faithful full 6-level pyramid),
     threads over contiguous epoch ranges, on a bounded sample of the same synthetic workload.
 
@@ -1089,10 +1097,12 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
     # SURVEY 8d / BASELINE.md: N = every core of the host available to this run (Spark local[*],
     # Utils/SparkInitializer.java:44); --cpu-threads overrides
     threads = args.cpu_threads or avail
-    k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10, args.epochs)
+    first = sp if first is None else first
+    k = min(args.cpu_sample if C == 3 else args.cpu_sample // 10,
+            args.epochs if n_epochs is None else n_epochs)
     k1 = max(1, min(k // 25, 20000 if C == 3 else 2000))  # one-thread sample
-    host = raw[: sp * k + 2000].cpu().numpy()
-    pos = np.arange(sp, sp * (k + 1), sp, dtype=np.int64)
+    host = raw[: first + sp * k + 2000].cpu().numpy()
+    pos = np.arange(first, first + sp * k, sp, dtype=np.int64)
     cols = list(range(C))
 
     def run(h, p, faithful, nthreads):
@@ -1102,7 +1112,7 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
         return oracle.process_recording_fast(h, cols, [0.1] * C, p, nthreads=nthreads)
 
     def leg(n, faithful, nthreads, reps=5):
-        h = host[: sp * n + 2000]
+        h = host[: first + sp * n + 2000]
         run(h[: sp * 200 + 2000], pos[: min(200, n)], faithful, nthreads)
         times, feats = [], None
         for _ in range(reps):
@@ -1130,7 +1140,7 @@ def cpu_baseline(args, raw, gpu_out, ct, C, sp=FRAMES_PER_EPOCH):
         "cores": threads,
         "host_cores": cores_info,
         "kind": "port",
-        "sample": f"first {k} epochs of the rank-0 synthetic recording, C restatement of the "
+        "sample": f"first {k} epochs of the {what}, C restatement of the "
                   f"Java path (full 6-level pyramid), {threads} threads over contiguous ranges, "
                   f"median of 5 runs of {dt:.2f} s wall",
         "gpu_parity_on_sample": parity,

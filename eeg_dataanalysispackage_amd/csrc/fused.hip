@@ -339,6 +339,69 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 #ifndef EEGFX_RECHECK_ROWS
 #define EEGFX_RECHECK_ROWS 1
 #endif
+// fma numerics: each channel wave normalises and stores its own 16 features of every row from
+// registers (the row's sum of squares combined through LDS), and the guard's second stage runs on
+// all channel waves against the windows still staged (window_rows_fast); 0 (A/B builds): the rows
+// go through LDS and one wave normalises, guards and stores them (normalise_store)
+#ifndef EEGFX_REG_ROWS
+#define EEGFX_REG_ROWS 1
+#endif
+
+// The guard's second stage for channel `col` of the flagged rows of a sub-tile, by one channel
+// wave: the flagged rows (bit 8e of `flagged` = epoch e) share the wave, L = 64,
+// 32, 16 or 8 lanes per row for 1, 2, 3-4, 5-8 rows; each lane reads 512 / L consecutive frames of
+// its row's window as staged in LDS (segment s at 16 SEGQ s bytes past the epoch's misalignment)
+// and keeps the column's min and max raw sample; those two are decoded exactly as the kernel
+// decodes every sample (x = fl(fl(raw * r) - b) is monotone in raw), and X_c = max |x| is reduced
+// over the row's lanes.  Returns X_c^2 on the lane sub == 0 of each row's slot (0 elsewhere) and
+// the epoch of the lane's slot in *row (-1 for lanes without one).  delta, b: the misalignment
+// and baseline of the lane's epoch (lane >> 3), shuffled to the slot's epoch.
+template <int FB, int SEGQ, int EBYTES>
+__device__ __forceinline__ double channel_x2_rows(uint64_t flagged, const uint8_t* win, int col,
+                                                  float r, float b, int delta, int lane,
+                                                  int* row) {
+  uint32_t T = 0;
+  int k = 0;
+#pragma unroll
+  for (int e = 0; e < kSub; ++e)
+    if ((flagged >> (8 * e)) & 1ull) { T |= (uint32_t)e << (4 * k); ++k; }
+  const int sh = k <= 1 ? 6 : k <= 2 ? 5 : k <= 4 ? 4 : 3;  // log2(L)
+  const int j = lane >> sh, sub = lane & ((1 << sh) - 1);
+  const bool valid = j < k;
+  const int e = valid ? (int)((T >> (4 * j)) & 15u) : (int)(T & 15u);
+  const int de = __shfl(delta, 8 * e, 64);
+  const float be = __shfl(b, 8 * e, 64);
+  const uint8_t* p0 = win + e * EBYTES + de + 2 * col;
+  const int fpl = 512 >> sh;  // frames per lane, a multiple of 8: runs never cross a segment
+  const int f0 = sub * fpl;
+  int mn = 32767, mx = -32768;
+  for (int t = 0; t < fpl; t += 8) {  // uniform trip count
+    const int f = f0 + t;
+    const uint8_t* p = p0 + 16 * SEGQ * (f >> 6) + FB * (f & 63);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const int v0 = *(const int16_t*)(p + FB * i), v1 = *(const int16_t*)(p + FB * (i + 1));
+      mn = min(mn, min(v0, v1));
+      mx = max(mx, max(v0, v1));
+    }
+  }
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  // (min, max) decoded as one pair: packed fp32 multiply and add, each lane rounded as the scalar
+  // fl(fl(raw * r) - b)
+  f32x2 x = f32x2{(float)mn, (float)mx} * f32x2{r, r};
+  x = x + f32x2{-be, -be};
+  // maximum over the row's L lanes (|x| >= 0: its bit pattern orders like the value)
+  uint32_t u = __float_as_uint(fmaxf(fabsf(x.x), fabsf(x.y)));
+  u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0xB1, 0xF, 0xF, true));
+  u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x4E, 0xF, 0xF, true));
+  u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x141, 0xF, 0xF, true));
+  if (sh >= 4) u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x140, 0xF, 0xF, true));
+  if (sh >= 5) u = max(u, (uint32_t)__shfl_xor((int)u, 16, 64));
+  if (sh >= 6) u = max(u, (uint32_t)__shfl_xor((int)u, 32, 64));
+  const double X = (double)__uint_as_float(u);
+  *row = valid && sub == 0 ? e : -1;
+  return X * X;
+}
 template <int CT, int C, bool FAST, bool NT, int SUBS = EEGFX_WIN_SUBS>
 __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
@@ -349,6 +412,9 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
   __shared__ __attribute__((aligned(16))) uint32_t win_all[SUBS * kSub * G::ESTR];
   __shared__ double norm_all[SUBS * kSub];
   __shared__ double gx_all[FAST ? SUBS * kSub * C : 1];  // the guard's X^2 per signal (fma)
+  constexpr bool REG = FAST && EEGFX_REG_ROWS;
+  __shared__ double part_all[REG ? SUBS * kSub * C : 1];  // per-signal sums of squares (REG)
+  __shared__ double xs_all[REG ? SUBS * kSub * C : 1];    // measured X_c^2 of flagged rows (REG)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = SUBS > 1 ? wid / C : 0, w = SUBS > 1 ? wid - h * C : wid;  // sub-tile, channel
@@ -390,6 +456,83 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
     cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);
   }
 
+  if constexpr (REG) {
+    // Each channel wave keeps its 16 features of each row in registers: the row's sum of squares
+    // is the three channels' shares, combined through LDS in channel order (the same value in
+    // every wave), and every wave normalises and stores its own part -- 8 lines of 128 B, a6 then
+    // d6 of its channel -- so the staged windows stay intact for the guard's second stage, which
+    // then runs on all channel waves at once.
+    double* part = part_all + h * kSub * C;
+    double* xs = xs_all + h * kSub * C;
+    double q = __builtin_fma(a6, a6, d6 * d6);
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    q += __shfl_xor(q, 4, 64);
+    if (s == 0) part[el * C + w] = q;
+    __syncthreads();
+    double acc = part[el * C];
+#pragma unroll
+    for (int c = 1; c < C; ++c) acc += part[el * C + c];
+    bool fails = false;
+    if (EEGFX_GUARD && guard.total && s == 0 && mine) {
+      double sx = gx[el * C];
+#pragma unroll
+      for (int c = 1; c < C; ++c) sx += gx[el * C + c];
+      fails = guard_fails(acc, kGuardK2Collapsed, sx);
+    }
+    const uint64_t flagged = __ballot(fails);  // bit 8e; the same mask in every channel wave
+    uint64_t left = 0;
+    if (flagged) {  // uniform over the workgroup, rare
+      int row;
+      const double x2 = channel_x2_rows<G::FB, G::SEGQ, G::ESTR * 4>(
+          flagged, (const uint8_t*)win, col, r, b, delta, lane, &row);
+      if (row >= 0) xs[row * C + w] = x2;
+      __syncthreads();
+      bool f2 = false;
+      if (s == 0 && ((flagged >> (8 * el)) & 1ull)) {
+        double sx = xs[el * C];
+#pragma unroll
+        for (int c = 1; c < C; ++c) sx += xs[el * C + c];
+        f2 = guard_fails(acc, kGuardK2Collapsed, sx * (1.0 + 0x1p-20));
+      }
+      left = __ballot(f2);
+      if (w == 0 && lane == 0) {
+        guard_count_rechecked(guard, __popcll(flagged));
+        if (left) guard_count_recomputed(guard, (unsigned long long)__popcll(left));
+      }
+    }
+    const double inv = rsqrt_nr(acc);
+    if (mine && !((left >> (8 * el)) & 1ull)) {
+      double* o = out + (e0 + el) * F + w * 16 + s;
+      __builtin_nontemporal_store(a6 * inv, o);
+      __builtin_nontemporal_store(d6 * inv, o + 8);
+    }
+    if (left && w == 0) {
+      // the guard's rare path: each such row recomputed under EXACT from the recording by wave
+      // 0, the staged windows as scratch (every wave is done with them: the barrier above)
+      double* scratch = (double*)win;
+      double* rowbuf = scratch + 768;
+      for (uint64_t f = left; f; f &= f - 1) {
+        const int e = (__ffsll((unsigned long long)f) - 1) >> 3;
+        const int64_t B = wb[e0 + e] & ~(int64_t)1;  // byte offset of the window
+        const int64_t f0 = B / G::FB;
+        dwt8_exact_row_wave(
+            [&](int c, int k) {
+              const float rc = sel.res[c], bc = base[(e0 + e) * C + c];
+              const float v = f0 + k < n_frames
+                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
+                                  : 0.0f;
+              float y = v * rc;
+              y = y - bc;
+              return (double)y;
+            },
+            C, 16, scratch, rowbuf, lane);
+        for (int i = lane; i < F; i += 64) out[(e0 + e) * F + i] = rowbuf[i];
+        wave_sync();
+      }
+    }
+    return;
+  }
   double* fb = (double*)win;
   __syncthreads();  // every wave has read its samples: the rows may overwrite the window
   // the row slot is recomputed here from an opaque copy of the lane id, so its address is not

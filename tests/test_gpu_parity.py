@@ -326,6 +326,26 @@ def test_streamed_equals_resident(ctx, chunk, ordered):
     assert eq(got, oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos))
 
 
+@pytest.mark.parametrize("chunk", [787, 1600, 8192, 1 << 20])
+def test_streamed_rows_into_pinned_output(ctx, chunk):
+    """In position order into a pinned output (the bench's case): the same rows as the pageable
+    output and the oracle, the buffer's other bytes untouched."""
+    import torch
+    rng = np.random.default_rng(chunk + 5)
+    nf = 60000
+    raw = synth_raw(rng, nf, 3)
+    pos = np.sort(rng.integers(100, nf + 100, size=400))
+    pos[-1] = nf + 100
+    pinned = torch.full((pos.size + 2, 48), -7.0, dtype=torch.float64, pin_memory=True).numpy()
+    out = pinned[1:-1]
+    got = ctx.process_recording_streamed(raw, 3, [0, 1, 2], [0.1] * 3, pos, chunk_frames=chunk,
+                                         out=out)
+    assert eq(got, oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos))
+    assert eq(got, ctx.process_recording_streamed(raw, 3, [0, 1, 2], [0.1] * 3, pos,
+                                                  chunk_frames=chunk))
+    assert np.all(pinned[0] == -7.0) and np.all(pinned[-1] == -7.0)
+
+
 def test_streamed_pinned_source_and_wide_layout(ctx_fma):
     import torch
     rng = np.random.default_rng(77)
