@@ -78,8 +78,9 @@ def sgd_train(ctx: Context, X, y, num_iterations: int = DEFAULT_NUM_ITERATIONS,
     """LogisticRegressionWithSGD on the device; returns (weights, iterations_run).  X (n x d
     float64, host numpy or device torch) and y (n labels 0/1) may live on either side.
     mini_batch_fraction < 1 samples iteration i's mini-batch as MLlib's data.sample(false, f,
-    42 + i) over num_partitions Spark partitions (None: the host's hardware threads, Spark
-    local[*]; eegfx_logreg_sgd_train_partitioned)."""
+    42 + i) over num_partitions Spark partitions (None: the processors available to the process,
+    affinity and cgroup quota honoured, as Spark local[*]'s Runtime.availableProcessors();
+    eegfx_logreg_sgd_train_partitioned)."""
     return _train("eegfx_logreg_sgd_train", ctx, X, y, num_iterations, step_size, reg_param,
                   mini_batch_fraction, convergence_tol, initial_weights, num_partitions)
 

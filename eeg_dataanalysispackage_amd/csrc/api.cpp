@@ -17,6 +17,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <sched.h>
 #include <string>
 #include <utility>
 #include <vector>
@@ -494,6 +495,46 @@ void parallel_memcpy(void* dst, const void* src, size_t bytes) {
   }
   for (auto& x : th) x.join();
 }
+
+// The processors this process may run on, as the JVM's Runtime.availableProcessors() counts them
+// (Spark local[*]'s defaultParallelism, SparkInitializer.java:44): the affinity mask, capped by a
+// cgroup CPU quota (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us), at least 1.
+// std::thread::hardware_concurrency() counts every online CPU of the machine instead.
+int available_processors() {
+  int n = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  if (n < 1) n = (int)std::max(1u, std::thread::hardware_concurrency());
+  auto cap = [&](double quota, double period) {
+    if (quota > 0 && period > 0) n = std::min(n, std::max(1, (int)std::ceil(quota / period)));
+  };
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    double period = 0;
+    if (fscanf(f, "%31s %lf", q, &period) == 2 && strcmp(q, "max") != 0) cap(atof(q), period);
+    fclose(f);
+  } else if (FILE* fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    double quota = -1, period = 0;
+    if (fscanf(fq, "%lf", &quota) != 1) quota = -1;
+    fclose(fq);
+    if (FILE* fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(fp, "%lf", &period) != 1) period = 0;
+      fclose(fp);
+    }
+    cap(quota, period);
+  }
+  return n;
+}
+
+// Joins the threads it holds when it goes out of scope (an exception from emplace_back or from a
+// later call leaves no joinable std::thread behind, which would call std::terminate).
+struct Joiner {
+  std::vector<std::thread> th;
+  ~Joiner() {
+    for (auto& t : th)
+      if (t.joinable()) t.join();
+  }
+};
 
 // Host batches up to this many window bytes go through the zero-copy path of
 // eegfx_extract_features_f64 (about 64 epochs of 3 channels).
@@ -1226,9 +1267,15 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       for (int64_t i = 0; i < n; ++i) sorted_pos[(size_t)i] = pos[order[(size_t)i]];
       spos = sorted_pos.data();
     }
+    // The positions go up front on the context stream.  Measured slower (profiles/r06/): the
+    // kernels writing the rows straight into a pinned caller buffer instead of a download per
+    // chunk (8.84 against 7.2 ms per configs[4] step); a pageable position copy per chunk on the
+    // upload stream (9.5 ms: each one blocks the host behind every earlier upload); one position
+    // copy on the context stream behind the first chunk's frames (7.44-7.48 against 7.13-7.16);
+    // each pinned chunk as two halves on two upload streams (7.75-7.81 against 7.14).
     int64_t* d_pos = (int64_t*)ctx->pos.get(sizeof(int64_t) * (size_t)n);
-    // (The kernels writing the rows straight into a pinned caller buffer, instead of a download
-    // per chunk, was measured slower: 8.84 against 7.2 ms per configs[4] step, profiles/r06g/.)
+    HIP_CHECK(hipMemcpyAsync(d_pos, spos, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice,
+                             ctx->stream));
     double* d_out = (double*)ctx->out.get(sizeof(double) * (size_t)(n * F));
     (void)ctx->fused.get(fused_scratch_bytes(n, C));  // every chunk's baselines fit: no realloc
     // chunk buffers: 64 B front pad (the kernels round the first quad down by < 16 B) + data
@@ -1262,9 +1309,7 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
           ctx->mb_stop();
         for (int b = 0; b < 2; ++b) pin[b] = ctx->pin_chunk[b].get(cbytes);
       }
-      // the buffers' stream-ordered allocations (context stream) precede every upload
-      HIP_CHECK(hipEventRecord(ctx->copied[R - 1], ctx->stream));
-      HIP_CHECK(hipStreamWaitEvent(cs, ctx->copied[R - 1], 0));
+      ctx->drain();  // d_pos uploaded; buffers idle
       int64_t i = 0, k = 0;
       while (i < n) {
         const int b = (int)(k % R);
@@ -1283,10 +1328,6 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
           src = (const uint8_t*)pin[k & 1];
         }
         if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs));
-        // this chunk's marker positions behind its frames on the upload stream (one upload of
-        // every position first kept the link idle for ~0.1 ms at the start of each call)
-        HIP_CHECK(hipMemcpyAsync(d_pos + i, spos + i, sizeof(int64_t) * (size_t)(j - i),
-                                 hipMemcpyHostToDevice, cs));
         HIP_CHECK(hipEventRecord(copied[b], cs));
         HIP_CHECK(hipStreamWaitEvent(ctx->stream, copied[b], 0));
         // frame f of the recording lives at raw_dev + f*FB for lo <= f < hi (pointer arithmetic
@@ -1344,8 +1385,11 @@ static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double
     if (!X || !y) fail(EEGFX_EINVAL, "null X / y");
     if (d < 1 || d > kLrMaxFeatures) fail(EEGFX_EINVAL, "d=%d outside [1, %d]", d, kLrMaxFeatures);
     if (num_iterations < 0) fail(EEGFX_EINVAL, "num_iterations %d", num_iterations);
-    // BernoulliSampler's require: f in [0, 1] up to RandomSampler.roundingEpsilon
-    if (!(mini_batch_fraction >= -1e-6 && mini_batch_fraction <= 1.0 + 1e-6))
+    // RDD.sample's require(fraction >= 0.0), then BernoulliSampler's upper bound 1 up to
+    // RandomSampler.roundingEpsilon
+    if (!(mini_batch_fraction >= 0.0))
+      fail(EEGFX_EINVAL, "Negative fraction value: %g", mini_batch_fraction);
+    if (!(mini_batch_fraction <= 1.0 + 1e-6))
       fail(EEGFX_EINVAL, "Sampling fraction (%g) must be on interval [0, 1]", mini_batch_fraction);
     const bool sampled = mini_batch_fraction < 1.0;
     if (sampled && grad != kGradLogistic)
@@ -1387,19 +1431,28 @@ static int glm_sgd_train(int grad, eegfx_ctx* ctx, const double* X, const double
       std::vector<uint32_t> masks((size_t)(chunk * words));
       std::vector<int64_t> counts((size_t)chunk);
       uint32_t* dmask = (uint32_t*)ctx->lr_mask.get(sizeof(uint32_t) * masks.size());
+      const int T_max = std::min(64, available_processors());
       for (int i0 = 0; i0 < num_iterations; i0 += chunk) {
         const int k = std::min(chunk, num_iterations - i0);
         ctx->drain();  // the previous chunk's upload and iterations are done with both buffers
-        const int T = (int)std::max<unsigned>(1, std::min<unsigned>(
-            (unsigned)k, std::min(64u, std::thread::hardware_concurrency())));
-        std::vector<std::thread> pool;
-        for (int t = 0; t < T; ++t)
-          pool.emplace_back([&, t] {
-            for (int j = t; j < k; j += T)  // GradientDescent's i = i0 + j + 1, seed 42 + i
-              counts[j] = spark::sample_mask(n, mini_batch_fraction, num_partitions,
-                                             42 + (int64_t)(i0 + j + 1), &masks[(size_t)j * words]);
-          });
-        for (auto& th : pool) th.join();
+        if (i0 > 0) {  // converged (or stopped): the remaining iterations would be skipped
+          int32_t conv = 0;
+          HIP_CHECK(hipMemcpyAsync(&conv, &st->converged, sizeof(conv), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+          HIP_CHECK(hipStreamSynchronize(ctx->stream));
+          if (conv != 0) break;
+        }
+        const int T = std::max(1, std::min(k, T_max));
+        {
+          Joiner pool;
+          for (int t = 0; t < T; ++t)
+            pool.th.emplace_back([&, t] {
+              for (int j = t; j < k; j += T)  // GradientDescent's i = i0 + j + 1, seed 42 + i
+                counts[j] = spark::sample_mask(n, mini_batch_fraction, num_partitions,
+                                               42 + (int64_t)(i0 + j + 1),
+                                               &masks[(size_t)j * words]);
+            });
+        }
         HIP_CHECK(hipMemcpyAsync(dmask, masks.data(), sizeof(uint32_t) * (size_t)(k * words),
                                  hipMemcpyHostToDevice, ctx->stream));
         for (int j = 0; j < k; ++j)
@@ -1464,8 +1517,9 @@ int eegfx_logreg_sgd_train(eegfx_ctx* ctx, const double* X, const double* y, int
                            int32_t num_iterations, double step_size, double reg_param,
                            double mini_batch_fraction, double convergence_tol, double* weights,
                            int32_t* iterations_run, int mem) {
-  // Spark local[*] (SparkInitializer.java:44): defaultParallelism = the host's cores
-  const int32_t parts = (int32_t)std::max(1u, std::thread::hardware_concurrency());
+  // Spark local[*] (SparkInitializer.java:44): defaultParallelism = the processors available
+  // to the process (Runtime.availableProcessors(): affinity and cgroup quota honoured)
+  const int32_t parts = (int32_t)available_processors();
   return glm_sgd_train(kGradLogistic, ctx, X, y, n, d, num_iterations, step_size, reg_param,
                        mini_batch_fraction, convergence_tol, parts, weights, iterations_run, mem);
 }

@@ -110,6 +110,8 @@ def test_errors(ctx):
     y[7] = 1.0
     with pytest.raises(fx.EegfxError):
         clf.sgd_train(ctx, X, y, mini_batch_fraction=1.5)  # BernoulliSampler's require
+    with pytest.raises(fx.EegfxError, match="Negative fraction"):
+        clf.sgd_train(ctx, X, y, mini_batch_fraction=-1e-7)  # RDD.sample's require(f >= 0)
     with pytest.raises(fx.EegfxError):
         clf.sgd_train(ctx, X, y, mini_batch_fraction=0.5, num_partitions=0)
     with pytest.raises(fx.EegfxError):
