@@ -42,7 +42,7 @@ def bytes_per_epoch(ct, C):
 
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFS = 78.6                    # vendor fp64 vector spec (not in the guide)
-FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (profiles/r01/r01b_perf_study.json)
+FP64_FMA_MEASURED_TFS = 55.8                   # v_fma_f64 probe on this part (git show c3ab853:profiles/r01/r01b_perf_study.json)
 # fp64 filter-bank flops per channel: fma numerics run levels 1-5 as the collapsed 280-tap filter
 # (16 x 280 + level 6's 16 x 10 = 4,640 MAC, dwt8.h), EXACT the level-by-level a-path cascade
 # (5,120 MAC)
@@ -386,7 +386,7 @@ def main():
     traced(args.warmup, "warmup")
     torch.cuda.synchronize(dev)
     # Settle: the first ~25 launches after idle run at a clock that first overshoots, then sinks
-    # below and recovers to the power-capped steady state (step trace, profiles/r04c/driver_gap);
+    # below and recovers to the power-capped steady state (step trace, git show c3ab853:profiles/r04c/driver_gap);
     # a short --warmup would otherwise time that transient.  Reported, not counted as warmup.
     settle_steps, s0 = 0, time.perf_counter()
     while (time.perf_counter() - s0) * 1e3 < args.settle_ms:

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <sched.h>
@@ -67,25 +68,58 @@ struct DevBuf {
   }
 };
 
-// Grow-only pinned host buffer (hipHostMalloc: mapped into the device address space), for the
-// small-batch IFeatureExtraction path and the streamed path's host staging.  Only touched by the
-// owning context's calls, which synchronise before they return.  Kept across calls: hipHostFree
-// synchronises the whole device, which waits for any context's resident server (up to its 1 s
-// idle exit), so a buffer is freed only when it grows and when the context is destroyed.
+// Pinned host memory is never returned to the runtime while the process runs: hipHostFree (like
+// hipFree) synchronises the whole device, which waits for every resident per-epoch server of
+// every context (up to its 1 s idle exit) -- a context destroyed or a staging buffer grown on one
+// executor thread stalled every other thread's calls for a second (profiles/r06/dropin_threads).
+// Buffers go back to this process-wide pool instead and are reused by the next request of at
+// least their size with the same flags; the pool holds at most the peak of what was in use.
+struct PinnedPool {
+  std::mutex mu;
+  std::multimap<std::pair<unsigned, size_t>, void*> free;  // (flags, capacity) -> buffer
+  void* take(size_t bytes, unsigned flags, size_t* cap) {
+    bytes = std::max<size_t>(bytes, 64);
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free.lower_bound({flags, bytes});
+      if (it != free.end() && it->first.first == flags && it->first.second <= 2 * bytes + 65536) {
+        void* p = it->second;
+        *cap = it->first.second;
+        free.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, flags) != hipSuccess) {
+      (void)hipGetLastError();
+      fail(EEGFX_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+    }
+    *cap = bytes;
+    return p;
+  }
+  void give(void* p, size_t cap, unsigned flags) {
+    if (!p) return;
+    std::lock_guard<std::mutex> l(mu);
+    free.emplace(std::make_pair(flags, cap), p);
+  }
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool();  // never destroyed: buffers live to process exit
+  return *pool;
+}
+
+// Grow-only pinned host buffer (hipHostMalloc: mapped into the device address space, from
+// pinned_pool), for the small-batch IFeatureExtraction path and the streamed path's host staging.
+// Only touched by the owning context's calls, which synchronise before they return.
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
   void* get(size_t bytes) {
     if (bytes > cap) {
-      if (p) (void)hipHostFree(p);
+      pinned_pool().give(p, cap, hipHostMallocMapped);
       p = nullptr;
       cap = 0;
-      if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped) != hipSuccess) {
-        (void)hipGetLastError();
-        p = nullptr;
-        fail(EEGFX_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
-      }
-      cap = bytes;
+      p = pinned_pool().take(bytes, hipHostMallocMapped, &cap);
     }
     return p;
   }
@@ -96,7 +130,7 @@ struct PinBuf {
     return d;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    pinned_pool().give(p, cap, hipHostMallocMapped);
     p = nullptr;
     cap = 0;
   }
@@ -148,6 +182,7 @@ struct eegfx_ctx {
   // memory the kernels store 1 into; eegfx_ctx_synchronize reports and clears it.
   int* err_host = nullptr;
   int* err_dev = nullptr;
+  size_t err_cap = 0;  // pinned_pool capacity of err_host
   bool timing = false;
   // HIP event pairs bracketing each timed (dominant) kernel launch on the context stream, plus
   // the algorithmic bytes each launch moved; summed by eegfx_ctx_kernel_stats.
@@ -235,6 +270,7 @@ struct eegfx_ctx {
   hipStream_t mb_stream = nullptr;
   MailboxCmd* mb_host = nullptr;
   MailboxCmd* mb_dev = nullptr;
+  size_t mb_cap = 0;  // pinned_pool capacity of mb_host
   uint32_t mb_seq = 0;
   uint32_t mb_gen = 0;      // launch generation (MailboxCmd::alive)
   bool mb_live = false;     // launched and not stopped by the host (it may still have idled out)
@@ -414,8 +450,8 @@ bool eegfx_ctx::mb_ready() {
       int least = 0, greatest = 0;
       HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
       HIP_CHECK(hipStreamCreateWithPriority(&mb_stream, hipStreamNonBlocking, greatest));
-      HIP_CHECK(hipHostMalloc((void**)&mb_host, sizeof(MailboxCmd),
-                              hipHostMallocMapped | hipHostMallocCoherent));
+      mb_host = (MailboxCmd*)pinned_pool().take(
+          sizeof(MailboxCmd), hipHostMallocMapped | hipHostMallocCoherent, &mb_cap);
       memset(mb_host, 0, sizeof(MailboxCmd));
       HIP_CHECK(hipHostGetDevicePointer((void**)&mb_dev, mb_host, 0));
       mb_seq = 0;
@@ -455,7 +491,8 @@ bool eegfx_ctx::mb_ready() {
 void eegfx_ctx::release_mailbox() {
   const bool stopped = mb_stop();
   if (mb_stream && stopped && !mb_stuck) (void)hipStreamDestroy(mb_stream);
-  if (mb_host && stopped && !mb_stuck) (void)hipHostFree(mb_host);
+  if (mb_host && stopped && !mb_stuck)
+    pinned_pool().give(mb_host, mb_cap, hipHostMallocMapped | hipHostMallocCoherent);
   // a stuck server keeps its stream and command block (it still reads `stop` when it runs):
   // leaked rather than freed under a queued kernel
   mb_host = nullptr;
@@ -876,11 +913,13 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     HIP_CHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->stream = c->own;
     c->bind_buffers();
-    HIP_CHECK(hipHostMalloc((void**)&c->err_host, sizeof(int), hipHostMallocMapped));
+    c->err_host = (int*)pinned_pool().take(sizeof(int), hipHostMallocMapped, &c->err_cap);
     *c->err_host = 0;
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
-    HIP_CHECK(hipMalloc((void**)&c->guard_dev, eegfx_ctx::kGuardDevBytes));
-    HIP_CHECK(hipMemset(c->guard_dev, 0, eegfx_ctx::kGuardDevBytes));
+    // stream-ordered: no allocation or free of a context synchronises the device
+    HIP_CHECK(hipMallocAsync((void**)&c->guard_dev, eegfx_ctx::kGuardDevBytes, c->own));
+    HIP_CHECK(hipMemsetAsync(c->guard_dev, 0, eegfx_ctx::kGuardDevBytes, c->own));
+    HIP_CHECK(hipStreamSynchronize(c->own));
     *out = c.release();
   });
 }
@@ -1009,8 +1048,9 @@ int eegfx_ctx_destroy(eegfx_ctx* ctx) {
     ctx->release_buffers();
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->own);
-    if (ctx->err_host) (void)hipHostFree(ctx->err_host);
-    if (ctx->guard_dev) (void)hipFree(ctx->guard_dev);
+    pinned_pool().give(ctx->err_host, ctx->err_cap, hipHostMallocMapped);
+    if (ctx->guard_dev) (void)hipFreeAsync(ctx->guard_dev, ctx->own);
+    (void)hipStreamSynchronize(ctx->own);
     ctx->release_stream_resources();
     ctx->destroy_events();
     (void)hipStreamDestroy(ctx->own);
@@ -1098,8 +1138,8 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
         // directly: one launch and one stream sync, no DMA transfers (each costs a copy-engine
         // round trip) and no allocation once the context's staging has grown.  The rows are EXACT
         // under both numerics (kernels.hip small_epoch), so the fma guard does not count them.
-        // growing a pinned buffer frees the old one, which synchronises the device: stop the
-        // resident server first (the next request restarts it)
+        // a resident server reads the staging it was launched with: stop it before a growth
+        // (the next request restarts it on the new buffers)
         if (ctx->mb_live && ((size_t)n * C * row_w > ctx->pin_in.cap || out_bytes > ctx->pin_out.cap))
           ctx->mb_stop();
         double* hin = (double*)ctx->pin_in.get((size_t)n * C * row_w);
@@ -1304,9 +1344,7 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       return std::min(chunk_frames, std::max(c, std::max(chunk_frames / 4, 2 * kSpan)));
     };
     try {
-      if (!pinned) {  // the context's grow-only staging (a growth frees: stop our server first)
-        if (ctx->mb_live && cbytes > std::min(ctx->pin_chunk[0].cap, ctx->pin_chunk[1].cap))
-          ctx->mb_stop();
+      if (!pinned) {  // the context's grow-only staging (pinned_pool: growing it syncs nothing)
         for (int b = 0; b < 2; ++b) pin[b] = ctx->pin_chunk[b].get(cbytes);
       }
       ctx->drain();  // d_pos uploaded; buffers idle

@@ -131,7 +131,9 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
  * kernel launch or a stream synchronisation -- the same device code, the same rows (small
  * batches of more epochs stay on the launch path, which runs them in parallel).  It returns by itself after 1 s without a request (and is restarted by the next one), or
  * when disabled / the context is destroyed.  While it runs, a device-wide synchronisation
- * (hipDeviceSynchronize, hipFree, hipHostFree) waits for it: disable it before such calls.  Its
+ * (hipDeviceSynchronize, hipFree, hipHostFree) waits for it: disable it before such calls (the
+ * library makes none: its pinned buffers are pooled for the process, its device buffers are
+ * allocated and freed stream-ordered, so creating and destroying contexts never waits).  Its
  * stream has the highest priority, which keeps it on a hardware queue of its own (streams of one
  * priority share a few queues in order).  That pool has 4 queues, so at most 4
  * contexts of a process hold a server on one device at a time: a context enabled beyond that

@@ -60,6 +60,8 @@ struct Job {
   double per_call;
   int rc;
   int mailbox;
+  std::vector<double> lat;  // seconds per call
+  int resident;             // held a started server at the end of its calls
 };
 static void* worker(void* arg) {
   Job* j = (Job*)arg;
@@ -71,11 +73,18 @@ static void* worker(void* arg) {
   double out[48];
   for (int i = 0; i < 20; ++i)
     eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out, EEGFX_MEM_HOST);
+  j->lat.resize((size_t)j->reps);
   const double t0 = now_s();
-  for (int i = 0; i < j->reps; ++i)
+  for (int i = 0; i < j->reps; ++i) {
+    const double c0 = now_s();
     j->rc |= eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)(i % 11) * 2250, 1, 3, 8,
                                         512, 175, 16, out, EEGFX_MEM_HOST);
+    j->lat[(size_t)i] = now_s() - c0;
+  }
   j->per_call = (now_s() - t0) / j->reps;
+  int32_t en = 0, res = 0;
+  eegfx_ctx_get_mailbox(ctx, &en, &res);
+  j->resident = res;
   eegfx_ctx_destroy(ctx);
   return nullptr;
 }
@@ -223,22 +232,31 @@ int main(int argc, char** argv) {
            "\"rows_identical_to_launch_path\": %s, \"threads\": {",
            mb.med * 1e6, mb.p99 * 1e6, 1.0 / mb.med, mb11.med * 1e6, k / mb11.med,
            same ? "true" : "false");
-    const int Tm[3] = {2, 4, 8};
-    for (int ti = 0; ti < 3; ++ti) {
+    // T threads with a context each, every one asking for a server: at most 4 hold one (the
+    // highest-priority queue pool), the rest serve on the launch path; per-call latency over all
+    const int Tm[5] = {2, 4, 8, 16, 32};
+    for (int ti = 0; ti < 5; ++ti) {
       const int T = Tm[ti];
       std::vector<pthread_t> th((size_t)T);
-      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1});
+      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1, {}, 0});
       for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
       double agg = 0, mean = 0;
-      int rc = 0;
+      int rc = 0, resident = 0;
+      std::vector<double> all;
       for (int t = 0; t < T; ++t) {
         pthread_join(th[(size_t)t], nullptr);
         agg += 1.0 / jobs[(size_t)t].per_call;
         mean += jobs[(size_t)t].per_call / T;
         rc |= jobs[(size_t)t].rc;
+        resident += jobs[(size_t)t].resident;
+        all.insert(all.end(), jobs[(size_t)t].lat.begin(), jobs[(size_t)t].lat.end());
       }
-      printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, \"rc\": %d}",
-             ti ? ", " : "", T, 1.0 / mean, agg, rc);
+      std::sort(all.begin(), all.end());
+      printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, "
+             "\"resident_servers\": %d, \"median_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, "
+             "\"rc\": %d}",
+             ti ? ", " : "", T, 1.0 / mean, agg, resident, all[all.size() / 2] * 1e6,
+             all[(size_t)(all.size() * 0.99)] * 1e6, all.back() * 1e6, rc);
     }
     printf("}},\n");
   }
