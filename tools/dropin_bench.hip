@@ -62,6 +62,7 @@ struct Job {
   int mailbox;
   std::vector<double> lat;  // seconds per call
   int resident;             // held a started server at the end of its calls
+  pthread_barrier_t* bar;   // every thread starts together and holds its context to the end
 };
 static void* worker(void* arg) {
   Job* j = (Job*)arg;
@@ -74,6 +75,7 @@ static void* worker(void* arg) {
   for (int i = 0; i < 20; ++i)
     eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out, EEGFX_MEM_HOST);
   j->lat.resize((size_t)j->reps);
+  if (j->bar) pthread_barrier_wait(j->bar);
   const double t0 = now_s();
   for (int i = 0; i < j->reps; ++i) {
     const double c0 = now_s();
@@ -85,6 +87,7 @@ static void* worker(void* arg) {
   int32_t en = 0, res = 0;
   eegfx_ctx_get_mailbox(ctx, &en, &res);
   j->resident = res;
+  if (j->bar) pthread_barrier_wait(j->bar);  // resident_servers counts servers held at once
   eegfx_ctx_destroy(ctx);
   return nullptr;
 }
@@ -178,7 +181,7 @@ int main(int argc, char** argv) {
   for (int ti = 0; ti < 3; ++ti) {
     const int T = Ts[ti];
     std::vector<pthread_t> th((size_t)T);
-    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 0});
+    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 0, {}, 0, nullptr});
     for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
     double agg = 0, mean = 0;
     int rc = 0;
@@ -238,7 +241,9 @@ int main(int argc, char** argv) {
     for (int ti = 0; ti < 5; ++ti) {
       const int T = Tm[ti];
       std::vector<pthread_t> th((size_t)T);
-      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1, {}, 0});
+      pthread_barrier_t bar;
+      pthread_barrier_init(&bar, nullptr, (unsigned)T);
+      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1, {}, 0, &bar});
       for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
       double agg = 0, mean = 0;
       int rc = 0, resident = 0;
@@ -251,6 +256,7 @@ int main(int argc, char** argv) {
         resident += jobs[(size_t)t].resident;
         all.insert(all.end(), jobs[(size_t)t].lat.begin(), jobs[(size_t)t].lat.end());
       }
+      pthread_barrier_destroy(&bar);
       std::sort(all.begin(), all.end());
       printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, "
              "\"resident_servers\": %d, \"median_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, "
