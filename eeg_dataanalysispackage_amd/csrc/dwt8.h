@@ -612,6 +612,25 @@ __device__ __forceinline__ double group8_max(double v) {
   return fmax(v, __shfl_xor(v, 4, 64));
 }
 
+// A double moved across lanes by one DPP control (both halves), e.g. 0xB1 = xor 1, 0x4E = xor 2
+// within a quad, 0x141 = row_half_mirror (lane i <- 7 - i within 8): no LDS round trip and no
+// lane-address arithmetic, where __shfl_xor costs four VALU and two ds_bpermute per step.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+// The sum over an aligned group of 8 lanes, identical in all 8 (each step adds a pair of equal
+// partial sums in either order).
+__device__ __forceinline__ double group8_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  return v + dpp_f64<0x141>(v);
+}
+
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps
 // (relative error ~1e-16, inside the 1e-9 contract); v = 0 gives inf, so an all-zero row still
 // normalises to NaN as the reference's 0/0 does.
@@ -620,6 +639,13 @@ __device__ __forceinline__ double rsqrt_nr(double v) {
   r = r * __builtin_fma(-0.5 * v * r, r, 1.5);
   r = r * __builtin_fma(-0.5 * v * r, r, 1.5);
   return r;
+}
+// The same with one Newton step: relative error ~1e-13 from v_rsq_f64's ~2^-23 start, four orders
+// of magnitude inside the 0.5e-9 the guard leaves the normalisation (guard.h); the window kernel's
+// three channel waves each compute it (fused.hip), so the step saved is saved three times.
+__device__ __forceinline__ double rsqrt_nr1(double v) {
+  const double r = __builtin_amdgcn_rsq(v);
+  return r * __builtin_fma(-0.5 * v * r, r, 1.5);
 }
 
 // One level of the analysis low-pass over a whole wave under EXACT numerics: out[i] =

@@ -346,6 +346,10 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 #ifndef EEGFX_REG_ROWS
 #define EEGFX_REG_ROWS 1
 #endif
+// Newton steps after v_rsq_f64 in the register-rows normalisation (1; 2 in A/B builds)
+#ifndef EEGFX_RSQ_STEPS
+#define EEGFX_RSQ_STEPS 1
+#endif
 
 // The guard's second stage for channel `col` of the flagged rows of a sub-tile, by one channel
 // wave: the flagged rows (bit 8e of `flagged` = epoch e) share the wave, L = 64,
@@ -464,10 +468,7 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
     // then runs on all channel waves at once.
     double* part = part_all + h * kSub * C;
     double* xs = xs_all + h * kSub * C;
-    double q = __builtin_fma(a6, a6, d6 * d6);
-    q += __shfl_xor(q, 1, 64);
-    q += __shfl_xor(q, 2, 64);
-    q += __shfl_xor(q, 4, 64);
+    const double q = group8_sum(__builtin_fma(a6, a6, d6 * d6));
     if (s == 0) part[el * C + w] = q;
     __syncthreads();
     double acc = part[el * C];
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
         if (left) guard_count_recomputed(guard, (unsigned long long)__popcll(left));
       }
     }
-    const double inv = rsqrt_nr(acc);
+    const double inv = EEGFX_RSQ_STEPS == 1 ? rsqrt_nr1(acc) : rsqrt_nr(acc);
     if (mine && !((left >> (8 * el)) & 1ull)) {
       double* o = out + (e0 + el) * F + w * 16 + s;
       __builtin_nontemporal_store(a6 * inv, o);
