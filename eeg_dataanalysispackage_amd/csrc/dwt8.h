@@ -600,6 +600,139 @@ __device__ __forceinline__ void dwt8_collapsed_cascade_b64(Fetch2 fetch2, float 
       gbase, s, a6, d6);
 }
 
+// The same filter with 4 lanes per signal (fused.hip window4_kernel, an A/B build: 8.9 % fewer VALU
+// instructions than the pair form, 2.5 % slower with half the waves per CU; DESIGN_LOG.md §R6):
+// lane s owns samples 128 s + k, k < 128, and outputs a5[4 s .. 4 s + 3].  Its samples come in
+// groups of four, x_t = sample n + 32 t (t < 4), which meet the same nine taps T_n as a pair does,
+// and the group's update is the product T_n(w) X(w) with X(w) = x3 + w x2 + w^2 x1 + w^3 x0: twelve
+// partials P[m] (m = j + 3 - t), of which P[0..3] are the lane's own outputs (a5[4 s + 3 - m]),
+// P[4..7] lane s-1's and P[8..11] lane s-2's.  In block form, T_n = B0(w^3) + w B1(w^3) +
+// w^2 B2(w^3) as in the pair update, (B0 + w B1 + w^2 B2) X(w) = c0 + ... + w^5 c5 is evaluated at
+// w = 0, infinity, 1, -1, 2, -2 -- six products of three entries, 18 multiply-adds per group --
+// and interpolated once (toom6_finish).  The four evaluations of X cost eight operations (two
+// sums, two fma per pair of points), exact whenever the four samples' exponents lie within ~26 of
+// each other; tools/fma_bound.py models every one of them as rounded.  Per sample: 6.5 fp64
+// operations instead of the pair form's 7, and half as many lanes pay the per-signal finish,
+// level 6 and the row epilogue.  The bound is wider (guard.h kGuardK2Toom6, 2.16e-4 against
+// 7.02e-5): the interpolation divides by 3 and the +-2 points weigh the samples up to 8x.
+static __constant__ double kT6[kT6Rows * kT6Cols] = EEGFX_T6_TABLE;
+constexpr int kLanesPerSignal4 = 4;
+
+// The six-point update of group n into the 18 accumulators V[k][q] (k: the points 0, inf, 1, -1,
+// 2, -2; the table's constants carry the interpolation's 1/2 and 1/24).
+__device__ __forceinline__ void toom6_group(const double (&R)[kT6Cols], int n, double x0,
+                                            double x1, double x2, double x3, double (&V)[6][3]) {
+  const double E1 = x3 + x1, O1 = x2 + x0;
+  const double E2 = __builtin_fma(4.0, x1, x3), O2 = __builtin_fma(4.0, x0, x2);
+  const double X[6] = {x3, x0, E1 + O1, E1 - O1, __builtin_fma(2.0, O2, E2),
+                       __builtin_fma(-2.0, O2, E2)};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (k == 1 && n + 32 * (3 * q + 2) >= 280) continue;  // B2 past tap 279
+      V[k][q] = n == 0 ? X[k] * R[3 * k + q] : __builtin_fma(X[k], R[3 * k + q], V[k][q]);
+    }
+  }
+  // the group's updates complete here (one scheduling region per group, as toom_pair)
+  asm volatile("" : "+v"(V[0][0]), "+v"(V[0][1]), "+v"(V[0][2]), "+v"(V[1][0]), "+v"(V[1][1]),
+               "+v"(V[1][2]), "+v"(V[2][0]), "+v"(V[2][1]), "+v"(V[2][2]));
+  asm volatile("" : "+v"(V[3][0]), "+v"(V[3][1]), "+v"(V[3][2]), "+v"(V[4][0]), "+v"(V[4][1]),
+               "+v"(V[4][2]), "+v"(V[5][0]), "+v"(V[5][1]), "+v"(V[5][2]));
+}
+
+// Interpolation (per q: c0 = V0, c5 = Vinf, S1 = V1 + Vm1 = c0 + c2 + c4, D1 = V1 - Vm1 =
+// c1 + c3 + c5, V2 + Vm2 = (c0 + 4 c2 + 16 c4) / 12, V2 - Vm2 = (c1 + 4 c3 + 16 c5) / 6), the
+// twelve partials P[3 q + r] = c_r[q] + c_{r+3}[q-1], the one partial round (lanes s+1, s+2) that
+// completes a5[4 s .. 4 s + 3], and level 6: a6[2 s + i], d6[2 s + i], i < 2, from a5[4 s .. 4 s + 11].
+__device__ __forceinline__ void toom6_finish(const double (&V)[6][3], int gbase, int s,
+                                             double (&a6)[2], double (&d6)[2]) {
+  constexpr double kMinusThird = -1.0 / 3.0;
+  double c[6][3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double c0 = V[0][q], c5 = V[1][q];
+    const double S1 = V[2][q] + V[3][q], D1 = V[2][q] - V[3][q];
+    const double T2 = V[4][q] + V[5][q], U2 = V[4][q] - V[5][q];
+    const double c4 = __builtin_fma(S1, kMinusThird, __builtin_fma(c0, 0.25, T2));
+    const double c2 = (S1 - c0) - c4;
+    const double c3 = __builtin_fma(U2, 2.0, __builtin_fma(D1, kMinusThird, c5 * -5.0));
+    const double c1 = (D1 - c3) - c5;
+    c[0][q] = c0; c[1][q] = c1; c[2][q] = c2; c[3][q] = c3; c[4][q] = c4; c[5][q] = c5;
+  }
+  double P[12];
+#pragma unroll
+  for (int m = 0; m < 12; ++m) {
+    const int q = m / 3, r = m % 3;
+    P[m] = q == 0 ? c[r][0] : q == 3 ? c[r + 3][2] : c[r][q] + c[r + 3][q - 1];
+  }
+  const int src1 = gbase + ((s + 1) & (kLanesPerSignal4 - 1));
+  const int src2 = gbase + ((s + 2) & (kLanesPerSignal4 - 1));
+  double a5[12];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    a5[i] = (P[3 - i] + __shfl(P[7 - i], src1, 64)) + __shfl(P[11 - i], src2, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a5[4 + i] = __shfl(a5[i], src1, 64);
+    a5[8 + i] = __shfl(a5[i], src2, 64);
+  }
+  a6[0] = fir10<true, false>(a5);
+  a6[1] = fir10<true, false>(a5 + 2);
+  d6[0] = fir10<true, true>(a5);
+  d6[1] = fir10<true, true>(a5 + 2);
+}
+
+// fetch(k): raw sample k < 128 of the lane's quarter; decode(v0, v1, x0, x1) as in
+// dwt8_collapsed_core.
+template <typename Fetch, typename Decode>
+__device__ __forceinline__ void dwt8_toom6_core(Fetch fetch, Decode decode, int gbase, int s,
+                                                double (&a6)[2], double (&d6)[2]) {
+  dwt8_const_f64_ptr tab = (dwt8_const_f64_ptr)kT6;
+  asm volatile("" : "+s"(tab));  // scalar loads of the table
+  double V[6][3];
+  typedef decltype(+fetch(0)) Raw;
+  Raw vq[2][4];  // two groups ahead
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) vq[d][t] = fetch(d + 32 * t);
+#pragma unroll
+  for (int n = 0; n < 32; ++n) {
+    Raw v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = vq[n % 2][t];
+    if (n + 2 < 32) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vq[n % 2][t] = fetch(n + 2 + 32 * t);
+    }
+    double R[kT6Cols];  // scalar loads (rows held one group ahead measured slower: SGPR spills)
+#pragma unroll
+    for (int i = 0; i < kT6Cols; ++i) R[i] = tab[n * kT6Cols + i];
+    double x0, x1, x2, x3;
+    decode(v[0], v[1], x0, x1);
+    decode(v[2], v[3], x2, x3);
+    toom6_group(R, n, x0, x1, x2, x3, V);
+  }
+  toom6_finish(V, gbase, s, a6, d6);
+}
+
+// dwt8_toom6_core with the fused kernels' decode, (double)((float)v * r - b), a pair at a time.
+template <typename Fetch>
+__device__ __forceinline__ void dwt8_toom6_cascade(Fetch fetch, float r, float b, int gbase, int s,
+                                                   double (&a6)[2], double (&d6)[2]) {
+  const dwt8_f32x2 rr = {r, r}, bb = {b, b};
+  dwt8_toom6_core(
+      fetch,
+      [&](auto v0, auto v1, double& x0, double& x1) {
+        const dwt8_f32x2 v = {(float)v0, (float)v1};
+        const dwt8_f32x2 y = v * rr - bb;
+        x0 = (double)y.x;
+        x1 = (double)y.y;
+      },
+      gbase, s, a6, d6);
+}
+
 // The largest value of v over the 8 lanes of a signal group.
 __device__ __forceinline__ float group8_max(float v) {
   v = fmaxf(v, __shfl_xor(v, 1, 64));
@@ -629,6 +762,11 @@ __device__ __forceinline__ double group8_sum(double v) {
   v += dpp_f64<0xB1>(v);
   v += dpp_f64<0x4E>(v);
   return v + dpp_f64<0x141>(v);
+}
+// The same over an aligned group of 4 lanes.
+__device__ __forceinline__ double group4_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  return v + dpp_f64<0x4E>(v);
 }
 
 // 1 / sqrt(v) for the fma numerics' row normalisation: v_rsq_f64 refined by two Newton steps

@@ -262,24 +262,24 @@ struct DmaRows {
 // DMAs) before the first DMA, so the DMAs leave back to back; an epoch whose window lies wholly
 // inside the recording (bit 0 of its word clear) takes the unguarded path.  Returns whether some
 // quad of this lane could not be DMA'd (the window reaches past either end of the recording).
-template <int CT, int C, bool NT>
+template <int CT, int C, bool NT, int SUB = kSub>
 __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64_t nbytes,
                                           const int64_t* __restrict__ wb, int64_t e0, int ne,
                                           uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
   constexpr int PER_E = DmaRows<CT>::PER_E;
-  constexpr int NE = (kSub + C - 1) / C;
+  constexpr int NE = (SUB + C - 1) / C;
   int64_t W[NE];
 #pragma unroll
   for (int t = 0; t < NE; ++t) {  // unconditional (clamped) loads: one scalar round trip
-    const int e = w + t * C < kSub ? w + t * C : kSub - 1;
+    const int e = w + t * C < SUB ? w + t * C : SUB - 1;
     W[t] = wb[e0 + (e < ne ? e : ne - 1)];
   }
   bool need_fix = false;
 #pragma unroll
   for (int t = 0; t < NE; ++t) {
     const int e = w + t * C;
-    if (e >= kSub || e >= ne) continue;  // uniform
+    if (e >= SUB || e >= ne) continue;  // uniform
     const int64_t Bq = W[t] & ~(int64_t)15;
     const uint8_t* sb = raw + Bq;
     uint32_t* dst = win + e * G::ESTR;
@@ -304,13 +304,13 @@ __device__ __forceinline__ bool dma_issue(const uint8_t* __restrict__ raw, int64
 
 // Direct (non-DMA) fill of the quads dma_issue skipped (same wave -> epoch mapping): zero or
 // partial quads at either end of the recording.
-template <int CT, int C>
+template <int CT, int C, int SUB = kSub>
 __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64_t nbytes,
                                           const int64_t* __restrict__ wb, int64_t e0, int ne,
                                           uint32_t* win, int w, int lane, const DmaRows<CT>& rows) {
   using G = Geometry<CT>;
   constexpr int PER_E = DmaRows<CT>::PER_E;
-  for (int e = w; e < kSub; e += C) {
+  for (int e = w; e < SUB; e += C) {
     if (e >= ne) break;
     const int64_t Bq = wb[e0 + e] & ~(int64_t)15;
 #pragma unroll
@@ -352,29 +352,31 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 #endif
 
 // The guard's second stage for channel `col` of the flagged rows of a sub-tile, by one channel
-// wave: the flagged rows (bit 8e of `flagged` = epoch e) share the wave, L = 64,
-// 32, 16 or 8 lanes per row for 1, 2, 3-4, 5-8 rows; each lane reads 512 / L consecutive frames of
-// its row's window as staged in LDS (segment s at 16 SEGQ s bytes past the epoch's misalignment)
-// and keeps the column's min and max raw sample; those two are decoded exactly as the kernel
-// decodes every sample (x = fl(fl(raw * r) - b) is monotone in raw), and X_c = max |x| is reduced
-// over the row's lanes.  Returns X_c^2 on the lane sub == 0 of each row's slot (0 elsewhere) and
-// the epoch of the lane's slot in *row (-1 for lanes without one).  delta, b: the misalignment
-// and baseline of the lane's epoch (lane >> 3), shuffled to the slot's epoch.
-template <int FB, int SEGQ, int EBYTES>
+// wave: the flagged rows (bit LPS e of `flagged` = epoch e, LPS lanes per signal)
+// share the wave, L = 64, 32, 16, 8 or 4 lanes per row for 1, 2, 3-4, 5-8 or 9-16 rows; each lane
+// reads 512 / L consecutive frames of its row's window as staged in LDS (segment s at 16 SEGQ s
+// bytes past the epoch's misalignment) and keeps the column's min and max raw sample; those two
+// are decoded exactly as the kernel decodes every sample (x = fl(fl(raw * r) - b) is monotone in
+// raw), and X_c = max |x| is reduced over the row's lanes.  Returns X_c^2 on the lane sub == 0 of
+// each row's slot (0 elsewhere) and the epoch of the lane's slot in *row (-1 for lanes without
+// one).  delta, b: the misalignment and baseline of the lane's epoch (lane / LPS), shuffled to the
+// slot's epoch.
+template <int FB, int SEGQ, int EBYTES, int SUB = kSub, int LPS = 8>
 __device__ __forceinline__ double channel_x2_rows(uint64_t flagged, const uint8_t* win, int col,
                                                   float r, float b, int delta, int lane,
                                                   int* row) {
-  uint32_t T = 0;
+  static_assert(SUB * LPS == 64 && SUB <= 16, "one wave per channel, 4-bit epoch slots");
+  uint64_t T = 0;
   int k = 0;
 #pragma unroll
-  for (int e = 0; e < kSub; ++e)
-    if ((flagged >> (8 * e)) & 1ull) { T |= (uint32_t)e << (4 * k); ++k; }
-  const int sh = k <= 1 ? 6 : k <= 2 ? 5 : k <= 4 ? 4 : 3;  // log2(L)
+  for (int e = 0; e < SUB; ++e)
+    if ((flagged >> (LPS * e)) & 1ull) { T |= (uint64_t)e << (4 * k); ++k; }
+  const int sh = k <= 1 ? 6 : k <= 2 ? 5 : k <= 4 ? 4 : k <= 8 ? 3 : 2;  // log2(L)
   const int j = lane >> sh, sub = lane & ((1 << sh) - 1);
   const bool valid = j < k;
   const int e = valid ? (int)((T >> (4 * j)) & 15u) : (int)(T & 15u);
-  const int de = __shfl(delta, 8 * e, 64);
-  const float be = __shfl(b, 8 * e, 64);
+  const int de = __shfl(delta, LPS * e, 64);
+  const float be = __shfl(b, LPS * e, 64);
   const uint8_t* p0 = win + e * EBYTES + de + 2 * col;
   const int fpl = 512 >> sh;  // frames per lane, a multiple of 8: runs never cross a segment
   const int f0 = sub * fpl;
@@ -398,7 +400,7 @@ __device__ __forceinline__ double channel_x2_rows(uint64_t flagged, const uint8_
   uint32_t u = __float_as_uint(fmaxf(fabsf(x.x), fabsf(x.y)));
   u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0xB1, 0xF, 0xF, true));
   u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x4E, 0xF, 0xF, true));
-  u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x141, 0xF, 0xF, true));
+  if (sh >= 3) u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x141, 0xF, 0xF, true));
   if (sh >= 4) u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x140, 0xF, 0xF, true));
   if (sh >= 5) u = max(u, (uint32_t)__shfl_xor((int)u, 16, 64));
   if (sh >= 6) u = max(u, (uint32_t)__shfl_xor((int)u, 32, 64));
@@ -586,6 +588,121 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
   }
 }
 
+// fma numerics, 3-channel int16 recordings, A/B builds (-DEEGFX_WIN4=1): the six-point form with
+// 4 lanes per signal (dwt8.h dwt8_toom6_core).  A channel wave holds 16 epochs and a workgroup
+// (3 waves, wave w = channel w) a 16-epoch sub-tile: 51 KB of staged windows in window_kernel's
+// per-epoch layout, three workgroups per CU.  Each lane reads its 128 samples (two segments)
+// straight from LDS; the rows are normalised and stored from registers by every channel wave
+// (a6[2 s], a6[2 s + 1], d6[2 s], d6[2 s + 1] of its channel: two 16-byte stores per lane), and the
+// guard's second stage scans the staged windows on all channel waves.  8.9 % fewer VALU
+// instructions than window_kernel (SQ_INSTS_VALU) but 2.5 % slower per step: with half the waves
+// per CU the window DMA is no longer covered by other workgroups' work (the kernel without its DMA
+// runs in 0.56 ms); persistent forms that overlap the next sub-tile's DMA themselves measured
+// slower still (DESIGN_LOG.md §R6).
+#ifndef EEGFX_WIN4
+#define EEGFX_WIN4 0
+#endif
+constexpr int kSub4 = 16;  // epochs per sub-tile of window4_kernel (16 epochs x 4 lanes = 64 lanes)
+
+template <bool NT>
+__global__ __launch_bounds__(192, 3) void window4_kernel(
+    const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
+    const float* __restrict__ base, int64_t n, double* __restrict__ out, Guard guard) {
+  using G = Geometry<3>;
+  constexpr int C = 3, F = C * 16, SUB = kSub4, LPS = kLanesPerSignal4;
+  static_assert(SUB * LPS == 64, "one wave per channel");
+  __shared__ __attribute__((aligned(16))) uint32_t win[SUB * G::ESTR];
+  __shared__ double gx[SUB * C];    // the guard's a-priori X^2 per signal
+  __shared__ double part[SUB * C];  // per-signal sums of squares
+  __shared__ double xs[SUB * C];    // measured X_c^2 of flagged rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // channel
+  const int el = lane >> 2, s = lane & 3;
+  const int64_t nbytes = n_frames * G::FB;
+  const int col = sel.col[w];
+  const float r = sel.res[w];
+  const int64_t e0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * SUB;
+  const int64_t rest = n - e0;  // >= 1
+  const int ne = rest >= SUB ? SUB : (int)rest;
+  const bool mine = el < ne;
+  const int64_t ec = e0 + (mine ? el : ne - 1);
+  const float b_ld = base[ec * C + w];
+  const uint32_t w_ld = (uint32_t)wb[ec];
+  const DmaRows<3> rows(lane);
+  if (dma_issue<3, C, NT, SUB>(raw, nbytes, wb, e0, ne, win, w, lane, rows))
+    dma_fixup<3, C, SUB>(raw, nbytes, wb, e0, ne, win, w, lane, rows);
+  const float b = mine ? b_ld : 0.0f;
+  const int delta = mine ? (int)(w_ld & 14u) : 0;
+  if (EEGFX_GUARD && s == 0) gx[el * C + w] = guard_x2_int16(r, b);  // read after the barriers
+  dma_drain();
+  __syncthreads();
+
+  // samples 128 s + k of signal (epoch el, channel w): segment 2 s + k / 64, frame k % 64
+  const uint8_t* own = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col + 32 * G::SEGQ * s;
+  double a6[2], d6[2];
+  dwt8_toom6_cascade(
+      [&](int k) { return (int)*(const int16_t*)(own + 16 * G::SEGQ * (k >> 6) + G::FB * (k & 63)); },
+      r, b, lane & ~(LPS - 1), s, a6, d6);
+
+  const double q = group4_sum(__builtin_fma(
+      a6[0], a6[0], __builtin_fma(a6[1], a6[1], __builtin_fma(d6[0], d6[0], d6[1] * d6[1]))));
+  if (s == 0) part[el * C + w] = q;
+  __syncthreads();
+  const double acc = (part[el * C] + part[el * C + 1]) + part[el * C + 2];
+  bool fails = false;
+  if (EEGFX_GUARD && guard.total && s == 0 && mine)
+    fails = guard_fails(acc, kGuardK2Toom6, (gx[el * C] + gx[el * C + 1]) + gx[el * C + 2]);
+  const uint64_t flagged = __ballot(fails);  // bit 4e; the same mask in every channel wave
+  uint64_t left = 0;
+  if (flagged) {  // uniform over the workgroup, rare
+    int row;
+    const double x2 = channel_x2_rows<G::FB, G::SEGQ, G::ESTR * 4, SUB, LPS>(
+        flagged, (const uint8_t*)win, col, r, b, delta, lane, &row);
+    if (row >= 0) xs[row * C + w] = x2;
+    __syncthreads();
+    bool f2 = false;
+    if (s == 0 && ((flagged >> (LPS * el)) & 1ull))
+      f2 = guard_fails(acc, kGuardK2Toom6,
+                       ((xs[el * C] + xs[el * C + 1]) + xs[el * C + 2]) * (1.0 + 0x1p-20));
+    left = __ballot(f2);
+    if (w == 0 && lane == 0) {
+      guard_count_rechecked(guard, __popcll(flagged));
+      if (left) guard_count_recomputed(guard, (unsigned long long)__popcll(left));
+    }
+  }
+  const double inv = rsqrt_nr1(acc);
+  if (mine && !((left >> (LPS * el)) & 1ull)) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    f64x2* o = (f64x2*)(out + (e0 + el) * F + w * 16 + 2 * s);
+    __builtin_nontemporal_store(f64x2{a6[0] * inv, a6[1] * inv}, o);
+    __builtin_nontemporal_store(f64x2{d6[0] * inv, d6[1] * inv}, o + 4);
+  }
+  if (left && w == 0) {
+    // the guard's rare path: each such row recomputed under EXACT from the recording by wave 0,
+    // the staged windows as scratch (every wave is done with them: the barrier above)
+    double* scratch = (double*)win;
+    double* rowbuf = scratch + 768;
+    for (uint64_t f = left; f; f &= f - 1) {
+      const int e = (__ffsll((unsigned long long)f) - 1) / LPS;
+      const int64_t B = wb[e0 + e] & ~(int64_t)1;  // byte offset of the window
+      const int64_t f0 = B / G::FB;
+      dwt8_exact_row_wave(
+          [&](int c, int k) {
+            const float rc = sel.res[c], bc = base[(e0 + e) * C + c];
+            const float v = f0 + k < n_frames
+                                ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
+                                : 0.0f;
+            float y = v * rc;
+            y = y - bc;
+            return (double)y;
+          },
+          C, 16, scratch, rowbuf, lane);
+      for (int i = lane; i < F; i += 64) out[(e0 + e) * F + i] = rowbuf[i];
+      wave_sync();
+    }
+  }
+}
+
 }  // namespace dev
 
 // Non-temporal (streaming) reads when the average marker spacing n_frames / n leaves the regions
@@ -641,9 +758,19 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
   const float* bs = (const float*)scratch;
   const int64_t* words = (const int64_t*)((const uint8_t*)scratch + window_words_offset(n, C));
   (void)pos;  // read by launch_fused_baseline, which wrote the window words
+  const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
+  if (fast && EEGFX_WIN4) {
+    const dim3 g4((unsigned)((n + dev::kSub4 - 1) / dev::kSub4));
+    if (nt)
+      hipLaunchKernelGGL((dev::window4_kernel<true>), g4, dim3(192), 0, st, (const uint8_t*)raw,
+                         n_frames, sel, words, bs, n, out, guard);
+    else
+      hipLaunchKernelGGL((dev::window4_kernel<false>), g4, dim3(192), 0, st, (const uint8_t*)raw,
+                         n_frames, sel, words, bs, n, out, guard);
+    return hipGetLastError();
+  }
   constexpr int subs = EEGFX_WIN_SUBS;
   const dim3 g((unsigned)((n + dev::kSub * subs - 1) / (dev::kSub * subs)));
-  const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
 #define EEGFX_WIN(FA, NTV)                                                                   \
   hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192 * subs), 0, st,         \
                      (const uint8_t*)raw, n_frames, sel, words, bs, n, out, guard)

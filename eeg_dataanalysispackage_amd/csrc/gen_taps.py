@@ -17,6 +17,12 @@ B2[q] = H5[n + 96 q + 64] (0 past tap 279), row n of the table holds B0[0..2], B
 sum rounded once.  The direct form (A/B builds) follows: rows n < 32 of H5[n + 32 j], j < 8 (one
 64-byte scalar load), then the j = 8 column H5[256 + n] as a tail of 32 entries (zero past 279).
 
+The six-point form (dwt8.h dwt8_toom6_core, 4 lanes per signal) takes a lane's samples in groups
+of four (n, n + 32, n + 64, n + 96), the same nine taps of row n: with B(w) = B0 + w B1 + w^2 B2 it
+accumulates the products at w = 0, infinity, 1, -1, 2, -2; row n of its table holds B0[0..2],
+B2[0..2], B(1)[0..2] / 2, B(-1)[0..2] / 2, B(2)[0..2] / 24 and B(-2)[0..2] / 24 (18 doubles, 144
+bytes), each exact and rounded once.
+
 Run from anywhere:  python3 eeg_dataanalysispackage_amd/csrc/gen_taps.py  (rewrites the header;
 tests/test_taps.py checks the committed header against this generator).
 """
@@ -34,6 +40,7 @@ STRIDE = 1 << LEVELS      # 32
 ROWS = 32                 # sample offsets n of a pair (n, n + 32)
 COLS = 8                  # j = 0..7 per row; j = 8 in the tail
 TOOM = 12                 # B0[3], B2[3], (B0 + B1 + B2)/2 [3], (B0 - B1 + B2)/2 [3]
+TOOM6 = 18                # B0[3], B2[3], B(1)/2 [3], B(-1)/2 [3], B(2)/24 [3], B(-2)/24 [3]
 
 
 @functools.lru_cache(maxsize=None)
@@ -76,6 +83,22 @@ def toom_rows():
     return tuple(rows)
 
 
+@functools.lru_cache(maxsize=None)
+def toom6_rows():
+    """Rows n < 32 of the six-point form's constants (see the module docstring)."""
+    H = combined_taps()
+    h = lambda m: H[m] if m < len(H) else 0
+    rows = []
+    for n in range(ROWS):
+        b = [[Fraction(h(n + STRIDE * (3 * q + r))) for q in range(3)] for r in range(3)]
+        B = lambda w, q: b[0][q] + w * b[1][q] + w * w * b[2][q]
+        row = [b[0][q] for q in range(3)] + [b[2][q] for q in range(3)]
+        row += [B(1, q) / 2 for q in range(3)] + [B(-1, q) / 2 for q in range(3)]
+        row += [B(2, q) / 24 for q in range(3)] + [B(-2, q) / 24 for q in range(3)]
+        rows.append(tuple(float(v) for v in row))
+    return tuple(rows)
+
+
 def tap(n, j):
     """H5[n + 32 j] as the kernel reads it from the table (0 past 279)."""
     rows, tail = table()
@@ -89,6 +112,7 @@ def header_text():
         "// (WaveletTransform.java:126-137; exact rational composition of the 12-decimal taps, rounded",
         "// once).  Rows n < 32 of the four-point form's 12 constants (gen_taps.py), then the direct",
         "// form's rows n < 32 of H5[n + 32 j], j < 8, and its tail H5[256 + n] (0 past tap 279).",
+        "// EEGFX_T6_TABLE: rows n < 32 of the six-point form's 18 constants (gen_taps.py).",
         "#pragma once",
         "",
         "namespace eegfx {",
@@ -98,12 +122,18 @@ def header_text():
         "constexpr int kH5Direct = kH5Rows * kH5Cols, kH5DirectCols = %d;" % COLS,
         "constexpr int kH5Tail = kH5Direct + kH5Rows * kH5DirectCols;",
         "constexpr int kH5Size = kH5Tail + kH5Rows;",
+        "constexpr int kT6Rows = %d, kT6Cols = %d;" % (ROWS, TOOM6),
         "#define EEGFX_H5_TABLE \\",
     ]
     rows, tail = table()
     body = ["    " + ", ".join(float.hex(v) for v in row) for row in toom_rows()]
     body += ["    " + ", ".join(float.hex(v) for v in row) for row in rows]
     body += ["    " + ", ".join(float.hex(v) for v in tail[i:i + 8]) for i in range(0, ROWS, 8)]
+    lines.append("  { \\")
+    lines.append(", \\\n".join(body) + " \\")
+    lines.append("  }")
+    lines.append("#define EEGFX_T6_TABLE \\")
+    body = ["    " + ", ".join(float.hex(v) for v in row) for row in toom6_rows()]
     lines.append("  { \\")
     lines.append(", \\\n".join(body) + " \\")
     lines.append("  }")

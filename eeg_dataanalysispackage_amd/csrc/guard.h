@@ -35,9 +35,11 @@
 namespace eegfx {
 
 // tools/fma_bound.py (tests/test_taps.py checks these against it): the collapsed four-point filter
-// of the fused and batch kernels, and the level-by-level fma cascade of features_small_kernel.
+// of the batch and 32-channel kernels, the level-by-level fma cascade of features_small_kernel, and
+// the six-point form of window4_kernel (4 lanes per signal, A/B builds).
 constexpr double kGuardK2Collapsed = 7.02e-05;
 constexpr double kGuardK2Cascade = 1.62e-04;
+constexpr double kGuardK2Toom6 = 2.16e-04;
 
 // Device state of a guarded launch: `count` flagged rows so far and their epoch indices in `list`
 // (window_wide_kernel only: zeroed before the launch that fills it, capacity the launch's epochs),

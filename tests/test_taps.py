@@ -4,8 +4,8 @@ dwt8_collapsed_cascade (csrc/dwt8.h) runs levels 1-5 of the fe=dwt-8 pyramid
 (WaveletTransform.java:126-137) as one 280-tap filter at stride 32.  These
 checks pin the committed header to gen_taps.py, the table to the exact rational composition of
 the 12-decimal taps, and the kernel's lane algebra (ten partial sums per lane, four received from
-lanes s+1..s+4; each pair's update in the direct and in the four-point Toom form) to the
-level-by-level cascade of the oracle.
+lanes s+1..s+4; each pair's update in the direct and in the four-point Toom form; the six-point
+form of the 4-lanes-per-signal window kernel) to the level-by-level cascade of the oracle.
 """
 import ctypes
 import os
@@ -68,7 +68,8 @@ def test_lane_algebra_matches_the_cascade():
         for _lev in range(5):
             N = len(a)
             a = np.array([sum(h[t] * a[(2 * k + t) % N] for t in range(10)) for k in range(N // 2)])
-        for got in (_lane_model(x, tab), _toom_lane_model(x, gen_taps.toom_rows())):
+        for got in (_lane_model(x, tab), _toom_lane_model(x, gen_taps.toom_rows()),
+                    _toom6_lane_model(x, gen_taps.toom6_rows())):
             assert np.max(np.abs(got - a)) <= 1e-12 * np.max(np.abs(a))
 
 
@@ -97,6 +98,60 @@ def _toom_lane_model(x, rows):
         a5[2 * s] = P[s][1] + sum(P[(s + d) % 8][2 * d + 1] for d in range(1, 5))
         a5[2 * s + 1] = P[s][0] + sum(P[(s + d) % 8][2 * d] for d in range(1, 5))
     return a5
+
+
+def toom6_interpolate(V0, Vi, V1, Vm1, V2, Vm2):
+    """dwt8.h toom6_finish's interpolation of one q: the six coefficients c0..c5 of
+    (B0 + w B1 + w^2 B2)(x3 + w x2 + w^2 x1 + w^3 x0) from the products at 0, inf, 1, -1, 2, -2
+    (V1, Vm1 scaled by 1/2, V2, Vm2 by 1/24 through the table)."""
+    S1, D1 = V1 + Vm1, V1 - Vm1        # c0 + c2 + c4, c1 + c3 + c5
+    T2, U2 = V2 + Vm2, V2 - Vm2        # (c0 + 4 c2 + 16 c4) / 12, (c1 + 4 c3 + 16 c5) / 6
+    c0, c5 = V0, Vi
+    c4 = T2 - S1 / 3 + c0 / 4
+    c2 = S1 - c0 - c4
+    c3 = 2 * U2 - D1 / 3 - 5 * c5
+    c1 = D1 - c3 - c5
+    return [c0, c1, c2, c3, c4, c5]
+
+
+def _toom6_lane_model(x, rows):
+    """The six-point form with 4 lanes per signal: lane s owns samples 128 s + k; group n is the
+    samples n + 32 t, t < 4, against the nine taps of row n; twelve partials P[m] (m = j + 3 - t),
+    the lane's a5[4 s + i] = P_s[3 - i] + P_{s+1}[7 - i] + P_{s+2}[11 - i]."""
+    P = np.zeros((4, 12))
+    for s in range(4):
+        xs = x[128 * s:128 * s + 128]
+        acc = np.zeros((6, 3))  # V0, Vi, V1, Vm1, V2, Vm2
+        for n in range(32):
+            x0, x1, x2, x3 = (xs[n + 32 * t] for t in range(4))
+            E1, O1 = x3 + x1, x2 + x0
+            E2, O2 = 4 * x1 + x3, 4 * x0 + x2
+            X = [x3, x0, E1 + O1, E1 - O1, 2 * O2 + E2, -2 * O2 + E2]
+            R = rows[n]
+            for k in range(6):
+                for q in range(3):
+                    acc[k][q] += X[k] * R[3 * k + q]
+        c = [toom6_interpolate(*(acc[k][q] for k in range(6))) for q in range(3)]  # c[q][r]
+        for m in range(12):
+            q, r = divmod(m, 3)
+            P[s][m] = (c[q][r] if q < 3 else 0.0) + (c[q - 1][r + 3] if q > 0 else 0.0)
+    a5 = np.zeros(16)
+    for s in range(4):
+        for i in range(4):
+            a5[4 * s + i] = P[s][3 - i] + P[(s + 1) % 4][7 - i] + P[(s + 2) % 4][11 - i]
+    return a5
+
+
+def test_toom6_rows_are_exactly_rounded():
+    H = gen_taps.combined_taps()
+    h = lambda m: H[m] if m < 280 else 0
+    for n in range(32):
+        R = gen_taps.toom6_rows()[n]
+        for q in range(3):
+            b0, b1, b2 = (Fraction(h(n + 32 * (3 * q + r))) for r in range(3))
+            want = [b0, b2, (b0 + b1 + b2) / 2, (b0 - b1 + b2) / 2, (b0 + 2 * b1 + 4 * b2) / 24,
+                    (b0 - 2 * b1 + 4 * b2) / 24]
+            assert [R[3 * k + q] for k in range(6)] == [float(v) for v in want]
 
 
 def test_toom_rows_are_exactly_rounded():

@@ -127,6 +127,67 @@ def fma_collapsed():
     return lo, hi
 
 
+def fma_toom6():
+    """dwt8.h dwt8_toom6_core (the 3-channel window kernel, 4 lanes per signal): per group of four
+    samples the six evaluations X(0) = x3, X(inf) = x0, X(+-1) = (x3 + x1) +- (x2 + x0),
+    X(+-2) = fma(+-2, fma(4, x0, x2), fma(4, x1, x3)), 6 x 3 accumulators over 32 groups, the
+    interpolation (toom6_finish, in its operation order), three partials per a5 and level 6 as
+    fir10 with fma."""
+    H = gen_taps.combined_taps()
+    hh = lambda m: H[m] if m < len(H) else Fraction(0)
+    x = V(1.0)
+    E1, O1 = add(x, x), add(x, x)
+    X1 = add(E1, O1)
+    Xm1 = add(E1, O1)
+    E2, O2 = fma(x, Fraction(4), x), fma(x, Fraction(4), x)
+    X2 = fma(O2, Fraction(2), E2)
+    Xm2 = fma(O2, Fraction(-2), E2)
+    acc = {}
+    for n in range(32):
+        for q in range(3):
+            b0, b1, b2 = (Fraction(hh(n + 32 * (3 * q + r))) for r in range(3))
+            terms = (("V0", x, b0), ("Vi", x, b2), ("V1", X1, (b0 + b1 + b2) / 2),
+                     ("Vm1", Xm1, (b0 - b1 + b2) / 2), ("V2", X2, (b0 + 2 * b1 + 4 * b2) / 24),
+                     ("Vm2", Xm2, (b0 - 2 * b1 + 4 * b2) / 24))
+            for name, src, c in terms:
+                if name == "Vi" and n + 32 * (3 * q + 2) >= 280:
+                    continue
+                k = (name, q)
+                acc[k] = cmul(src, c) if k not in acc else fma(src, c, acc[k])
+    third = Fraction(-1, 3)
+    C = [[None] * 3 for _ in range(6)]
+    for q in range(3):
+        g = lambda k: acc[(k, q)]
+        c0, c5 = g("V0"), g("Vi")
+        S1, D1 = add(g("V1"), g("Vm1")), add(g("V1"), g("Vm1"))
+        T2, U2 = add(g("V2"), g("Vm2")), add(g("V2"), g("Vm2"))
+        c4 = fma(S1, third, fma(c0, Fraction(1, 4), T2))
+        c2 = add(add(S1, c0), c4)
+        c3 = fma(U2, Fraction(2), fma(D1, third, cmul(c5, Fraction(-5))))
+        c1 = add(add(D1, c3), c5)
+        for r, v in enumerate((c0, c1, c2, c3, c4, c5)):
+            C[r][q] = v
+    P = []
+    for m in range(12):
+        q, r = divmod(m, 3)
+        if q == 0:
+            P.append(C[r][0])
+        elif q == 3:
+            P.append(C[r + 3][2])
+        else:
+            P.append(add(C[r][q], C[r + 3][q - 1]))
+    a5 = V(0.0)
+    for i in range(4):  # a5[4s + i] = (P_s[3 - i] + P_s+1[7 - i]) + P_s+2[11 - i]
+        t = add(add(P[3 - i], P[7 - i]), P[11 - i])
+        a5 = V(max(a5.m, t.m), max(a5.e, t.e))
+    lo = cmul(a5, LIT[0])
+    hi = cmul(a5, ghigh(0))
+    for j in range(1, 10):
+        lo = fma(a5, LIT[j], lo)
+        hi = fma(a5, ghigh(j), hi)
+    return lo, hi
+
+
 def fma_cascade():
     """dwt8_cascade<true> (features_small_kernel under fma): level-by-level fir10 with fma; the
     partial-sum halos of levels 2-5 split a chain between two lanes without adding roundings, and
@@ -153,7 +214,8 @@ def constants(tol=0.5e-9, safety=1.25):
     features_small_kernel)."""
     ex_lo, ex_hi = exact_cascade()
     out = dict(exact_a6=ex_lo.e, exact_d6=ex_hi.e, tol=tol, safety=safety)
-    for name, (lo, hi) in (("collapsed", fma_collapsed()), ("cascade", fma_cascade())):
+    for name, (lo, hi) in (("collapsed", fma_collapsed()), ("cascade", fma_cascade()),
+                           ("toom6", fma_toom6())):
         Ea, Ed = ex_lo.e + lo.e, ex_hi.e + hi.e
         out[name + "_a6"], out[name + "_d6"] = lo.e, hi.e
         out[name + "_E_a6"], out[name + "_E_d6"] = Ea, Ed
@@ -165,7 +227,7 @@ if __name__ == "__main__":
     c = constants()
     for k, v in c.items():
         print("%-16s %.6e" % (k, v))
-    for name in ("collapsed", "cascade"):
+    for name in ("collapsed", "cascade", "toom6"):
         k2 = c[name + "_k2"]
         print("%-9s per-row threshold: |f|^2 >= %.6e * sum_c X_c^2  (|f| >= %.4e * sqrt(sum X_c^2))"
               % (name, k2, k2 ** 0.5))
