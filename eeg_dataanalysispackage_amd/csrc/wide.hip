@@ -367,7 +367,27 @@ struct C32Shared {
   double norm1;
   double gx[C32::C];  // the guard's X^2 per channel (fma numerics)
   int redo;
+  double part[4];     // per-wave sums of squares (EEGFX_C32_REG)
+  double gxw[4];      // per-wave sums of the guard's X^2 (EEGFX_C32_REG)
 };
+
+// fma numerics, A/B builds: 1 = every lane normalises and stores its own a6, d6 from registers (the row's sum
+// of squares from per-wave DPP / cross-lane sums combined through LDS, one barrier), the
+// features through LDS only for a row the guard flags; 0 = the features through LDS, wave 0 sums
+// and tests the row and every thread stores 16 bytes of it (the product: the register form measured
+// 2.0 % slower, 2.044 vs 2.000 ms per launch, profiles/r06/c32_reg_ab.log -- the cross-lane sums
+// cost more than wave 0's pass over the row).
+#ifndef EEGFX_C32_REG
+#define EEGFX_C32_REG 0
+#endif
+
+// The sum over the wave's 64 lanes (the same value in all of them).
+__device__ __forceinline__ double wave_sum64(double v) {
+  v = group8_sum(v);
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
 
 // Filter bank, normalisation and store of epoch e from its staged window (published by a
 // barrier); this lane's channel c = 8 w + lane / 8 has column col_c, resolution r and baseline b
@@ -403,11 +423,40 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
     dwt8_levels2to6<FAST, true>(a1, nullptr, lane & ~7, s, a6, d6);
   }
   double* feat = sh.feat;
-  feat[c * 16 + s] = a6;
-  feat[c * 16 + 8 + s] = d6;
-  if (FAST && EEGFX_GUARD && s == 0) sh.gx[c] = guard_x2_int16(r, b);
-  __syncthreads();
   double* o = out + e * F;
+  if constexpr (FAST && EEGFX_C32_REG) {
+    const double q = wave_sum64(__builtin_fma(a6, a6, d6 * d6));
+    const double gq = wave_sum64(EEGFX_GUARD && s == 0 ? guard_x2_int16(r, b) : 0.0);
+    if (lane == 0) {
+      sh.part[w] = q;
+      sh.gxw[w] = gq;
+    }
+    if (EEGFX_GUARD && s == 0) sh.gx[c] = guard_x2_int16(r, b);  // for the rare path below
+    __syncthreads();
+    const double acc = ((sh.part[0] + sh.part[1]) + sh.part[2]) + sh.part[3];
+    const double sx = ((sh.gxw[0] + sh.gxw[1]) + sh.gxw[2]) + sh.gxw[3];
+    const bool fails = EEGFX_GUARD && guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
+    if (!fails) {  // uniform: every lane stores its two features
+      const double inv = rsqrt_nr1(acc);
+      if constexpr (STREAM) {
+        __builtin_nontemporal_store(a6 * inv, o + c * 16 + s);
+        __builtin_nontemporal_store(d6 * inv, o + c * 16 + 8 + s);
+      } else {
+        o[c * 16 + s] = a6 * inv;
+        o[c * 16 + 8 + s] = d6 * inv;
+      }
+      return;
+    }
+    // the guard's second stage and rare recompute, as below, from the features in LDS
+    feat[c * 16 + s] = a6;
+    feat[c * 16 + 8 + s] = d6;
+    __syncthreads();
+  } else {
+    feat[c * 16 + s] = a6;
+    feat[c * 16 + 8 + s] = d6;
+    if (FAST && EEGFX_GUARD && s == 0) sh.gx[c] = guard_x2_int16(r, b);
+    __syncthreads();
+  }
   if constexpr (FAST) {
     if (w == 0) {
       double acc = 0.0;
