@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "dwt8.h"
 #include "guard.h"
@@ -378,18 +379,30 @@ __device__ __forceinline__ double channel_x2_rows(uint64_t flagged, const uint8_
   const int de = __shfl(delta, LPS * e, 64);
   const float be = __shfl(b, LPS * e, 64);
   const uint8_t* p0 = win + e * EBYTES + de + 2 * col;
-  const int fpl = 512 >> sh;  // frames per lane, a multiple of 8: runs never cross a segment
-  const int f0 = sub * fpl;
   int mn = 32767, mx = -32768;
-  for (int t = 0; t < fpl; t += 8) {  // uniform trip count
-    const int f = f0 + t;
-    const uint8_t* p = p0 + 16 * SEGQ * (f >> 6) + FB * (f & 63);
+  // FPL = 512 / L frames per lane (a multiple of 8: runs never cross a segment), one fully unrolled
+  // scan per row count so that every read of a lane is in flight before the first min / max
+  auto scan = [&](auto fplc) {
+    constexpr int FPL = decltype(fplc)::value;
+    const int f0 = sub * FPL;
 #pragma unroll
-    for (int i = 0; i < 8; i += 2) {
-      const int v0 = *(const int16_t*)(p + FB * i), v1 = *(const int16_t*)(p + FB * (i + 1));
-      mn = min(mn, min(v0, v1));
-      mx = max(mx, max(v0, v1));
+    for (int t = 0; t < FPL; t += 8) {
+      const int f = f0 + t;
+      const uint8_t* p = p0 + 16 * SEGQ * (f >> 6) + FB * (f & 63);
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const int v0 = *(const int16_t*)(p + FB * i), v1 = *(const int16_t*)(p + FB * (i + 1));
+        mn = min(mn, min(v0, v1));
+        mx = max(mx, max(v0, v1));
+      }
     }
+  };
+  switch (sh) {  // uniform
+    case 6: scan(std::integral_constant<int, 8>()); break;
+    case 5: scan(std::integral_constant<int, 16>()); break;
+    case 4: scan(std::integral_constant<int, 32>()); break;
+    case 3: scan(std::integral_constant<int, 64>()); break;
+    default: scan(std::integral_constant<int, 128>()); break;
   }
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   // (min, max) decoded as one pair: packed fp32 multiply and add, each lane rounded as the scalar
