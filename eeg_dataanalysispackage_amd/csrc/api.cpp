@@ -11,6 +11,7 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -35,6 +36,11 @@ using namespace eegfx;
     hipError_t _e = (expr);                                                             \
     if (_e != hipSuccess) fail(EEGFX_EHIP, "%s: %s", #expr, hipGetErrorString(_e));     \
   } while (0)
+
+// Microseconds a small call's waiter spins before it sleeps (A/B builds vary it).
+#ifndef EEGFX_SMALL_SPIN_US
+#define EEGFX_SMALL_SPIN_US 30
+#endif
 
 namespace {
 
@@ -242,16 +248,21 @@ struct eegfx_ctx {
     }
   }
   // Completion of a small (latency-bound) call: spinning on an event query returns ~0.5 us sooner
-  // than hipStreamSynchronize (the drop-in bench's launch floor: 11.6 vs 12.2 us); after 200 us
-  // the wait blocks instead, so a busy device does not keep the calling thread spinning.
+  // than hipStreamSynchronize (the drop-in bench's launch floor: 11.6 vs 12.2 us).  Past kSmallSpin
+  // the thread sleeps until the event completes (a blocking-sync event: interrupt-driven), so a
+  // waiter is not runnable: with more calling threads than cores (Spark local[*] on a CPU quota),
+  // runnable waiters kept threads whose work had completed off the cores for scheduler slices
+  // (profiles/r06/dropin_gate_ab.log).
+  static constexpr auto kSmallSpin = std::chrono::microseconds(EEGFX_SMALL_SPIN_US);
   hipEvent_t small_done = nullptr;
   void wait_small() {
-    if (!small_done) HIP_CHECK(hipEventCreateWithFlags(&small_done, hipEventDisableTiming));
+    if (!small_done)
+      HIP_CHECK(hipEventCreateWithFlags(&small_done, hipEventDisableTiming | hipEventBlockingSync));
     HIP_CHECK(hipEventRecord(small_done, stream));
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
     while ((e = hipEventQuery(small_done)) == hipErrorNotReady) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+      if (std::chrono::steady_clock::now() - t0 > kSmallSpin) {
         HIP_CHECK(hipEventSynchronize(small_done));
         return;
       }
@@ -334,6 +345,9 @@ struct eegfx_ctx {
     __atomic_store_n(&m->req, mailbox_request(mb_seq, C, nfeat, n), __ATOMIC_RELEASE);
     for (uint64_t spin = 1;; ++spin) {
       if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == mb_seq) break;
+      // as wait_small: a waiter past kSmallSpin sleeps between polls instead of staying runnable
+      if ((spin & 63) == 0 && std::chrono::steady_clock::now() - now > kSmallSpin)
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
       if ((spin & 4095) == 0) {
         // a server that returned with the request pending (an error, or a stop from another
         // path): serve it again on the same stream, after that kernel
@@ -426,6 +440,39 @@ void mb_release(int dev) {
   std::lock_guard<std::mutex> l(g_mb_mu);
   if (dev >= 0 && dev < kMbMaxDevices && g_mb_used[dev] > 0) --g_mb_used[dev];
 }
+
+// Admission of small launched calls (one epoch per call from many threads, no server): at most
+// kSmallCallers per device are inside the runtime at once, the others sleep on a condition
+// variable and are admitted in arrival order (tickets).  Without it 28 threads launching and
+// waiting on one device (Spark local[*] with 32 executor threads, 4 of them on servers) convoyed
+// in the runtime: calls of 42-48 ms (profiles/r06/dropin_gate_ab.log; A/B builds vary the cap).
+#ifndef EEGFX_SMALL_CALLERS
+#define EEGFX_SMALL_CALLERS 8
+#endif
+constexpr int kSmallCallers = EEGFX_SMALL_CALLERS;
+std::mutex g_small_mu;
+std::condition_variable g_small_cv;
+uint64_t g_small_ticket[kMbMaxDevices] = {};  // tickets issued
+uint64_t g_small_done[kMbMaxDevices] = {};    // calls that have left
+struct SmallCallGate {
+  int dev;
+  explicit SmallCallGate(int d) : dev(d >= 0 && d < kMbMaxDevices ? d : -1) {
+    if (dev < 0 || kSmallCallers <= 0) return;
+    std::unique_lock<std::mutex> l(g_small_mu);
+    const uint64_t t = g_small_ticket[dev]++;
+    g_small_cv.wait(l, [&] { return t < g_small_done[dev] + (uint64_t)kSmallCallers; });
+  }
+  ~SmallCallGate() {
+    if (dev < 0 || kSmallCallers <= 0) return;
+    {
+      std::lock_guard<std::mutex> l(g_small_mu);
+      ++g_small_done[dev];
+    }
+    g_small_cv.notify_all();
+  }
+  SmallCallGate(const SmallCallGate&) = delete;
+  SmallCallGate& operator=(const SmallCallGate&) = delete;
+};
 
 }  // namespace
 
@@ -1155,6 +1202,7 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
           memcpy(out, hout, out_bytes);
           return;
         }
+        SmallCallGate gate(ctx->device);
         ctx->tic();
         HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
                                         feature_size, (double*)ctx->pin_out.device_ptr()));

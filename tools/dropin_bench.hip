@@ -257,6 +257,20 @@ int main(int argc, char** argv) {
         all.insert(all.end(), jobs[(size_t)t].lat.begin(), jobs[(size_t)t].lat.end());
       }
       pthread_barrier_destroy(&bar);
+      // the slowest calls (stderr): thread, call index, whether that thread held a server
+      for (int rank = 0; rank < 3; ++rank) {
+        int bt = -1, bi = -1;
+        double bv = -1;
+        for (int t = 0; t < T; ++t)
+          for (size_t i = 0; i < jobs[(size_t)t].lat.size(); ++i)
+            if (jobs[(size_t)t].lat[i] > bv) { bv = jobs[(size_t)t].lat[i]; bt = t; bi = (int)i; }
+        if (bt < 0) break;
+        fprintf(stderr, "threads %d slowest #%d: %.1f us (thread %d call %d resident %d)\n", T, rank,
+                bv * 1e6, bt, bi, jobs[(size_t)bt].resident);
+        jobs[(size_t)bt].lat[(size_t)bi] = -jobs[(size_t)bt].lat[(size_t)bi];
+      }
+      for (int t = 0; t < T; ++t)
+        for (double& v : jobs[(size_t)t].lat) v = v < 0 ? -v : v;
       std::sort(all.begin(), all.end());
       printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, "
              "\"resident_servers\": %d, \"median_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, "
