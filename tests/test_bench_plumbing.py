@@ -28,7 +28,7 @@ def test_traffic_reader_takes_the_newest_summary():
     names = sorted((f for f in os.listdir(pdir) if f.endswith(".json") and "traffic" in f and
                     json.load(open(os.path.join(pdir, f))).get("workload_key") == key),
                    key=bench.run_tag_order)
-    assert names[-1].startswith("r06z_")  # the newest run (round 6)
+    assert names[-1].startswith("r06zz_")  # the newest run (round 6)
     assert got == json.load(open(os.path.join(pdir, names[-1])))
     # FETCH_SIZE x2 (gfx950) + WRITE_SIZE over the algorithmic 3,476 B per epoch: a few % over
     assert 1.0 <= got["hbm_bytes_per_launch"] / 3.476e9 < 1.1
