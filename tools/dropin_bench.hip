@@ -230,6 +230,50 @@ int main(int argc, char** argv) {
       return a == b || (a != a && b != b);
     });
     CK(eegfx_ctx_set_mailbox(ctx, 0));
+    // where the served context's launched batches lose time: the same launched calls on this
+    // context (server stopped) while ANOTHER context keeps a server resident
+    eegfx_ctx* ctx2 = nullptr;
+    CK(eegfx_ctx_create(0, &ctx2));
+    CK(eegfx_ctx_set_mailbox(ctx2, 1));
+    for (int i = 0; i < 50; ++i)
+      CK(eegfx_extract_features_f64(ctx2, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                    EEGFX_MEM_HOST));
+    int32_t en2 = 0, res2 = 0;
+    CK(eegfx_ctx_get_mailbox(ctx2, &en2, &res2));
+    lat.clear();
+    for (int i = 0; i < reps / 4; ++i) {
+      const double t0 = now_s();
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data(), k, 3, 8, 512, 175, 16, got11.data(),
+                                    EEGFX_MEM_HOST));
+      lat.push_back(now_s() - t0);
+      if (i % 64 == 0)  // keep the other server inside its idle window
+        CK(eegfx_extract_features_f64(ctx2, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                      EEGFX_MEM_HOST));
+    }
+    const Lat other11 = stats(lat);
+    lat.clear();
+    for (int i = 0; i < reps / 4; ++i) {
+      const double t0 = now_s();
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                    EEGFX_MEM_HOST));
+      lat.push_back(now_s() - t0);
+      if (i % 64 == 0)
+        CK(eegfx_extract_features_f64(ctx2, g_epochs.data(), 1, 3, 8, 512, 175, 16, out,
+                                      EEGFX_MEM_HOST));
+    }
+    const Lat other1 = stats(lat);
+    CK(eegfx_ctx_destroy(ctx2));
+    lat.clear();
+    for (int i = 0; i < reps / 4; ++i) {  // and with no server anywhere, again
+      const double t0 = now_s();
+      CK(eegfx_extract_features_f64(ctx, g_epochs.data(), k, 3, 8, 512, 175, 16, got11.data(),
+                                    EEGFX_MEM_HOST));
+      lat.push_back(now_s() - t0);
+    }
+    const Lat none11 = stats(lat);
+    printf(" \"launched_beside_a_server\": {\"other_context_resident\": %d, \"batch_11_median_us\": %.2f, "
+           "\"single_median_us\": %.2f, \"batch_11_no_server_median_us\": %.2f},\n",
+           res2, other11.med * 1e6, other1.med * 1e6, none11.med * 1e6);
     printf(" \"mailbox\": {\"single_epoch\": {\"median_us\": %.2f, \"p99_us\": %.2f, "
            "\"epochs_per_s\": %.1f}, \"batch_11\": {\"median_us\": %.2f, \"epochs_per_s\": %.1f}, "
            "\"rows_identical_to_launch_path\": %s, \"threads\": {",
