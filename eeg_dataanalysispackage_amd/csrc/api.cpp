@@ -189,6 +189,14 @@ struct eegfx_ctx {
   int* err_host = nullptr;
   int* err_dev = nullptr;
   size_t err_cap = 0;  // pinned_pool capacity of err_host
+  // the fma window kernel's guard strategy (guard.h EEGFX_TRACK_X), set by baseline_kernel in the
+  // same host-mapped block, 8 bytes past the error word
+  unsigned int* track_host() const { return (unsigned int*)((char*)err_host + 8); }
+  unsigned int* track_dev() const { return (unsigned int*)((char*)err_dev + 8); }
+  bool guard_track() const {
+    return EEGFX_TRACK_X == 2 ||
+           (EEGFX_TRACK_X == 1 && __atomic_load_n(track_host(), __ATOMIC_RELAXED) != 0);
+  }
   bool timing = false;
   // HIP event pairs bracketing each timed (dominant) kernel launch on the context stream, plus
   // the algorithmic bytes each launch moved; summed by eegfx_ctx_kernel_stats.
@@ -203,7 +211,7 @@ struct eegfx_ctx {
   // of the current window_wide_kernel launch (first 128 B), then the running totals of recomputed
   // rows and of rows that went to the second stage, each spread over kGuardSlots lines; the
   // flagged-row list; guard_checked counts the rows that went through a guarded launch.
-  static constexpr size_t kGuardDevBytes = 128 + 2 * kGuardSlotBytes;
+  static constexpr size_t kGuardDevBytes = 128 + 2 * kGuardSlotBytes + 128;  // + Guard::adapt
   int* guard_dev = nullptr;
   DevBuf guard_list;
   int64_t guard_checked = 0;
@@ -213,11 +221,14 @@ struct eegfx_ctx {
   unsigned long long* guard_rechecked_slots() const {
     return (unsigned long long*)((char*)guard_dev + 128 + kGuardSlotBytes);
   }
+  unsigned long long* guard_adapt() const {
+    return (unsigned long long*)((char*)guard_dev + 128 + 2 * kGuardSlotBytes);
+  }
   Guard guard_for(int64_t n) {
     if (numerics == EEGFX_EXACT) return Guard{nullptr, nullptr, nullptr};
     guard_checked += n;
     return Guard{guard_dev, (int64_t*)guard_list.get(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1)),
-                 guard_recomputed_slots(), guard_rechecked_slots()};
+                 guard_recomputed_slots(), guard_rechecked_slots(), guard_adapt(), track_dev()};
   }
   void bind_buffers() {
     for (DevBuf* b : {&raw, &pos, &out, &scratch, &fused, &lr_x, &lr_y, &lr_state, &lr_part,
@@ -641,10 +652,10 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   if (fused_supported(fmt, ct, C, out)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_fused_baseline(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fscratch,
-                                    ctx->err_dev, nullptr));
+                                    ctx->err_dev, nullptr, fast ? &g : nullptr));
     ctx->tic();  // the dominant kernel (DESIGN.md "Measurement")
     HIP_CHECK(launch_fused_window(ctx->stream, raw, n_frames, ct, sel, C, pos, n, fast, fscratch,
-                                  out, g));
+                                  out, g, fast && ctx->guard_track()));
     ctx->toc(n * fused_window_bytes_per_epoch(ct, C));
     return;
   }
@@ -960,8 +971,8 @@ int eegfx_ctx_create(int device, eegfx_ctx** out) {
     HIP_CHECK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->stream = c->own;
     c->bind_buffers();
-    c->err_host = (int*)pinned_pool().take(sizeof(int), hipHostMallocMapped, &c->err_cap);
-    *c->err_host = 0;
+    c->err_host = (int*)pinned_pool().take(16, hipHostMallocMapped, &c->err_cap);
+    memset(c->err_host, 0, 16);  // the error word, then (+8) the guard strategy word
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
     // stream-ordered: no allocation or free of a context synchronises the device
     HIP_CHECK(hipMallocAsync((void**)&c->guard_dev, eegfx_ctx::kGuardDevBytes, c->own));

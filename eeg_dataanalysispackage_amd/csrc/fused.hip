@@ -143,7 +143,8 @@ template <int CT, int C, int TILE, bool STREAM = false>
 __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ pos,
     int64_t n, float* __restrict__ bout, int64_t* __restrict__ wout, int* __restrict__ err,
-    int* __restrict__ guard_count) {
+    int* __restrict__ guard_count, const unsigned long long* __restrict__ rechecked,
+    unsigned long long* __restrict__ adapt, unsigned int* __restrict__ track_out) {
   using G = Geometry<CT>;
   constexpr int NT = (TILE * C + 63) / 64 * 64;
   __shared__ __attribute__((aligned(16))) uint32_t stage[TILE * G::BSTR];
@@ -154,6 +155,25 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
   // a window kernel that follows may append to the guard list (fma numerics)
   if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
+  // the window kernel's guard strategy for this launch (Guard::adapt): track when the previous
+  // launch sent more than 1/16 of its rows to the second stage; a reset of the counters (total
+  // below the last one seen) keeps the strategy
+  if (adapt && rechecked && blockIdx.x == 0 && tid < 64) {
+    unsigned long long t = 0;
+    for (int i = tid; i < kGuardSlots; i += 64) t += rechecked[i * kGuardSlotWords];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    if (tid == 0) {
+      const unsigned long long snap = adapt[1], nprev = adapt[2];
+      unsigned long long mode = adapt[0];
+      if (t >= snap) mode = nprev > 0 && (t - snap) * 16 > nprev ? 1ull : 0ull;
+      adapt[0] = mode;
+      adapt[1] = t;
+      adapt[2] = (unsigned long long)n;
+      if (track_out)  // host-mapped: the host launches the next window kernel accordingly
+        __hip_atomic_store(track_out, (unsigned int)mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   if (tid < TILE) {
     const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
     if (!position_ok(p, n_frames)) flag_position(err);
@@ -210,12 +230,16 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
 // nxt[k*CT] of the next segment.
 // FMA numerics: dwt8_fast_cascade (own samples only; partial-sum halos); EXACT: level1_exact
 // (own samples; the 8 level-1 halo samples as decoded doubles from lane s+1) and value halos.
-template <int CT, bool FAST>
+template <int CT, bool FAST, bool TRACK = false>
 __device__ __forceinline__ void cascade_lds(const int16_t* own, const int16_t* nxt, float r,
-                                            float b, int gbase, int s, double& a6, double& d6) {
+                                            float b, int gbase, int s, double& a6, double& d6,
+                                            float* ymax = nullptr) {
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
-    if constexpr (EEGFX_LDS_B64 && CT == 3) {
+    if constexpr (TRACK) {
+      dwt8_collapsed_cascade<true>([&](int k) { return (float)own[k * CT]; }, r, b, gbase, s, a6,
+                                   d6, ymax);
+    } else if constexpr (EEGFX_LDS_B64 && CT == 3) {
       typedef uint64_t u64_a2 __attribute__((aligned(2)));
       dwt8_collapsed_cascade_b64([&](int k) { return *(const u64_a2*)(own + k * CT); }, r, b,
                                  gbase, s, a6, d6);
@@ -351,6 +375,7 @@ __device__ __forceinline__ void dma_fixup(const uint8_t* __restrict__ raw, int64
 #ifndef EEGFX_RSQ_STEPS
 #define EEGFX_RSQ_STEPS 1
 #endif
+// EEGFX_TRACK_X (guard.h): the guard's second-stage strategy of the fma window kernel.
 
 // The guard's second stage for channel `col` of the flagged rows of a sub-tile, by one channel
 // wave: the flagged rows (bit LPS e of `flagged` = epoch e, LPS lanes per signal)
@@ -421,7 +446,7 @@ __device__ __forceinline__ double channel_x2_rows(uint64_t flagged, const uint8_
   *row = valid && sub == 0 ? e : -1;
   return X * X;
 }
-template <int CT, int C, bool FAST, bool NT, int SUBS = EEGFX_WIN_SUBS>
+template <int CT, int C, bool FAST, bool NT, int SUBS = EEGFX_WIN_SUBS, bool TRK = false>
 __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel, const int64_t* __restrict__ wb,
     const float* __restrict__ base, int64_t n, double* __restrict__ out, Guard guard) {
@@ -468,11 +493,16 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
 
   // this lane's 64 samples + 8 halo samples of signal (epoch el, channel w), decoded in level 1
   double a6 = 0.0, d6 = 0.0;
+  // TRK: this launch tracks max |x| (EEGFX_TRACK_X, guard.h) -- a variant of its own, so the
+  // scanning launches carry no second filter loop
+  constexpr bool TRACKABLE = FAST && TRK && EEGFX_REG_ROWS && EEGFX_GUARD;
+  constexpr bool track = TRACKABLE;  // (no flag is raised without guard.total either way)
+  float ymax = 0.0f;
   if (SUBS == 1 || ne > 0) {
     const uint8_t* eb = (const uint8_t*)(win + el * G::ESTR) + delta + 2 * col;
     const int16_t* own = (const int16_t*)(eb + 16 * G::SEGQ * s);
     const int16_t* nxt = (const int16_t*)(eb + 16 * G::SEGQ * ((s + 1) & 7));
-    cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);
+    cascade_lds<CT, FAST, TRACKABLE>(own, nxt, r, b, lane & ~7, s, a6, d6, &ymax);
   }
 
   if constexpr (REG) {
@@ -484,6 +514,15 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
     double* part = part_all + h * kSub * C;
     double* xs = xs_all + h * kSub * C;
     const double q = group8_sum(__builtin_fma(a6, a6, d6 * d6));
+    if constexpr (track) {
+      // the signal's measured X_c = max |x| over its 8 lanes (|x| >= 0 orders like its bits)
+      uint32_t u = __float_as_uint(ymax);
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0xB1, 0xF, 0xF, true));
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x4E, 0xF, 0xF, true));
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x141, 0xF, 0xF, true));
+      const double X = (double)__uint_as_float(u);
+      if (s == 0) xs[el * C + w] = X * X;
+    }
     if (s == 0) part[el * C + w] = q;
     __syncthreads();
     double acc = part[el * C];
@@ -498,7 +537,20 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
     }
     const uint64_t flagged = __ballot(fails);  // bit 8e; the same mask in every channel wave
     uint64_t left = 0;
-    if (flagged) {  // uniform over the workgroup, rare
+    if (track && flagged) {  // the measured X_c of every row is already in LDS
+      bool f2 = false;
+      if (s == 0 && ((flagged >> (8 * el)) & 1ull)) {
+        double sx = xs[el * C];
+#pragma unroll
+        for (int c = 1; c < C; ++c) sx += xs[el * C + c];
+        f2 = guard_fails(acc, kGuardK2Collapsed, sx * (1.0 + 0x1p-20));
+      }
+      left = __ballot(f2);
+      if (w == 0 && lane == 0) {
+        guard_count_rechecked(guard, __popcll(flagged));
+        if (left) guard_count_recomputed(guard, (unsigned long long)__popcll(left));
+      }
+    } else if (flagged) {  // uniform over the workgroup, rare
       int row;
       const double x2 = channel_x2_rows<G::FB, G::SEGQ, G::ESTR * 4>(
           flagged, (const uint8_t*)win, col, r, b, delta, lane, &row);
@@ -746,7 +798,10 @@ int64_t fused_window_bytes_per_epoch(int ct, int C) {
 
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 void* scratch, int* err, int* guard_count) {
+                                 void* scratch, int* err, int* guard_count, const Guard* guard) {
+  const unsigned long long* rechecked = guard ? guard->rechecked : nullptr;
+  unsigned long long* adapt = guard && guard->total ? guard->adapt : nullptr;
+  unsigned int* track_out = adapt ? guard->track_out : nullptr;
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
   // 64 epochs per workgroup; 16/32/128 measured the same or slower.  Streaming
@@ -756,16 +811,17 @@ hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_fram
   if (streaming_reads(n_frames, n, dev::kPre + 687))
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64, true>), g, dim3(192), 0, st,
                        (const uint8_t*)raw, n_frames, sel, pos, n, (float*)scratch, words, err,
-                       guard_count);
+                       guard_count, rechecked, adapt, track_out);
   else
     hipLaunchKernelGGL((dev::baseline_kernel<3, 3, 64>), g, dim3(192), 0, st, (const uint8_t*)raw,
-                       n_frames, sel, pos, n, (float*)scratch, words, err, guard_count);
+                       n_frames, sel, pos, n, (float*)scratch, words, err, guard_count, rechecked,
+                       adapt, track_out);
   return hipGetLastError();
 }
 
 hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                               const void* scratch, double* out, const Guard& guard) {
+                               const void* scratch, double* out, const Guard& guard, bool track) {
   if (ct != 3 || C != 3) return hipErrorNotSupported;
   if (n == 0) return hipSuccess;
   const float* bs = (const float*)scratch;
@@ -784,11 +840,13 @@ hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames
   }
   constexpr int subs = EEGFX_WIN_SUBS;
   const dim3 g((unsigned)((n + dev::kSub * subs - 1) / (dev::kSub * subs)));
-#define EEGFX_WIN(FA, NTV)                                                                   \
-  hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV>), g, dim3(192 * subs), 0, st,         \
+#define EEGFX_WIN(FA, NTV, TK)                                                               \
+  hipLaunchKernelGGL((dev::window_kernel<3, 3, FA, NTV, subs, TK>), g, dim3(192 * subs), 0, st, \
                      (const uint8_t*)raw, n_frames, sel, words, bs, n, out, guard)
-  if (fast) { if (nt) EEGFX_WIN(true, true); else EEGFX_WIN(true, false); }
-  else { if (nt) EEGFX_WIN(false, true); else EEGFX_WIN(false, false); }
+  const bool trk = EEGFX_TRACK_X != 0 && (EEGFX_TRACK_X == 2 || track) && guard.total;
+  if (fast && trk) { if (nt) EEGFX_WIN(true, true, true); else EEGFX_WIN(true, false, true); }
+  else if (fast) { if (nt) EEGFX_WIN(true, true, false); else EEGFX_WIN(true, false, false); }
+  else { if (nt) EEGFX_WIN(false, true, false); else EEGFX_WIN(false, false, false); }
 #undef EEGFX_WIN
   return hipGetLastError();
 }

@@ -58,7 +58,28 @@ struct Guard {
   int64_t* list;
   unsigned long long* total;
   unsigned long long* rechecked = nullptr;
+  // the 3-channel window kernel's guard strategy (fused.hip, EEGFX_TRACK_X): adapt[0] = 1 when
+  // the previous launch sent more than 1/16 of its rows to the second stage (every lane then
+  // tracks max |x| while decoding, so no row needs the scan), set by baseline_kernel from
+  // adapt[1] (the rechecked total it last saw) and adapt[2] (that launch's rows); may be null
+  unsigned long long* adapt = nullptr;
+  // host-mapped word that baseline_kernel sets to the strategy it chose from adapt (the host picks
+  // the window kernel's variant for its next launch from it); may be null
+  unsigned int* track_out = nullptr;
 };
+
+// The guard's second stage in the fma 3-channel window kernel (fused.hip), two strategies:
+//   scan   the a-priori int16 bound for every row, and a scan of the staged windows for the rows
+//          it flags (channel_x2_rows): free while few rows are flagged;
+//   track  every lane keeps the largest |x| of the samples it decodes (one v_max3_f32 per pair,
+//          +3 % per step), so every row has its measured X_c and no flagged row needs the scan
+//          (+0.8 % at a 32 % flag rate, where the scan costs +8 %).
+// 1 (product) = adaptive: the host launches the tracking variant when the last launch's
+// baseline_kernel found that the launch before sent more than 1/16 of its rows to the second
+// stage; 0 = always scan, 2 = always track (A/B builds).
+#ifndef EEGFX_TRACK_X
+#define EEGFX_TRACK_X 1
+#endif
 
 namespace dev {
 

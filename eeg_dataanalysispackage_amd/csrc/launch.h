@@ -85,10 +85,12 @@ size_t fused_scratch_bytes(int64_t n, int C);
 // the rows that fail the fma conditioning guard itself and uses guard.total only).
 hipError_t launch_fused_baseline(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                  const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                                 void* scratch, int* err, int* guard_count);
+                                 void* scratch, int* err, int* guard_count,
+                                 const Guard* guard = nullptr);
 hipError_t launch_fused_window(hipStream_t st, const void* raw, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                               const void* scratch, double* out, const Guard& guard);
+                               const void* scratch, double* out, const Guard& guard,
+                               bool track = false);
 // Algorithmic HBM bytes per epoch of window_kernel (the dominant kernel): window frames, the
 // baseline and marker position it reads, the feature row it writes.
 int64_t fused_window_bytes_per_epoch(int ct, int C);

@@ -314,6 +314,35 @@ def test_flat_and_null_windows_mixed(ctx):
     assert redone == len(null) and rechecked == len(null) + len(flat)
 
 
+def test_guard_strategies_agree():
+    """The 3-channel window kernel's two second-stage strategies (fused.hip EEGFX_TRACK_X): a
+    context's first launch scans the staged windows of the rows it flags; a launch after one that
+    flagged more than 1/16 of its rows tracks max |x| while decoding instead.  Flat rows (certified)
+    and null-space rows (recomputed) mixed: both launches give the same rows, counters and oracle
+    values, and the strategy survives a counter reset."""
+    c = fx.Context(0, numerics="fma")
+    n = 48
+    raw, pos, flat = flat_recording(n, 1000, 3, 2)
+    raw = raw.astype(np.int64)
+    null = np.arange(1, n, 4)
+    alt = np.where(np.arange(-100, 750) % 2 == 0, 1, -1)[:, None] * 90 - 3000
+    for k in null:
+        raw[pos[k] - 100:pos[k] + 750] = alt
+    raw = raw.astype(np.int16)
+    want = oracle.process_recording(raw, [0, 1, 2], [0.1] * 3, pos)
+    runs = []
+    for _ in range(3):  # scan, then track (and track again after the reset)
+        c.guard_detail(reset=True)
+        got = c.process_recording(raw, 3, [0, 1, 2], [0.1] * 3, pos)
+        runs.append((got, c.guard_detail()))
+    for got, (checked, rechecked, redone) in runs:
+        assert within(got, want)
+        assert eq(got[null], want[null])
+        assert checked == n and redone == len(null) and rechecked == len(null) + len(flat)
+    assert eq(runs[0][0], runs[1][0]) and eq(runs[1][0], runs[2][0])
+    c.close()
+
+
 def test_exact_numerics_not_guarded():
     c = fx.Context(0)  # EXACT
     raw = alternating(12000, 3, 5, 0)

@@ -84,7 +84,7 @@ ABLATIONS = {
         "no window DMA, no LDS sample reads (wrong results)",
         [("fused.hip", DMA_ISSUE,
           "    (void)rows;  // ablation: no LDS staging; the lane's 64 samples come from VGPRs"),
-         ("fused.hip", """    cascade_lds<CT, FAST>(own, nxt, r, b, lane & ~7, s, a6, d6);""",
+         ("fused.hip", """    cascade_lds<CT, FAST, TRACKABLE>(own, nxt, r, b, lane & ~7, s, a6, d6, &ymax);""",
           """    (void)own; (void)nxt;
     u32x4_a4 q[8];
     {
