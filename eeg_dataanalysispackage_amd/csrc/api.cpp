@@ -1055,8 +1055,10 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
   return guarded([&] {
     if (!ctx || !rows_checked || !rows_recomputed) fail(EEGFX_EINVAL, "null argument");
     ctx->activate();
-    std::vector<unsigned long long> slots(2 * kGuardSlots * kGuardSlotWords);
-    HIP_CHECK(hipMemcpyAsync(slots.data(), ctx->guard_recomputed_slots(), 2 * kGuardSlotBytes,
+    // the two slot arrays and, right behind them, Guard::adapt (strategy, rechecked offset, rows)
+    std::vector<unsigned long long> slots(2 * kGuardSlots * kGuardSlotWords + 3);
+    HIP_CHECK(hipMemcpyAsync(slots.data(), ctx->guard_recomputed_slots(),
+                             2 * kGuardSlotBytes + 3 * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, ctx->stream));
     ctx->drain();
     unsigned long long tot[2] = {0, 0};  // recomputed, rechecked
@@ -1066,7 +1068,12 @@ int eegfx_ctx_guard_detail(eegfx_ctx* ctx, int64_t* rows_checked, int64_t* rows_
     *rows_recomputed = (int64_t)tot[0];
     if (rows_rechecked) *rows_rechecked = (int64_t)tot[1];
     if (reset) {
+      // the adaptive strategy's offset moves with the cleared total (fused.hip baseline_kernel)
+      const unsigned long long off =
+          (unsigned long long)((long long)slots[2 * kGuardSlots * kGuardSlotWords + 1] - (long long)tot[1]);
       HIP_CHECK(hipMemsetAsync(ctx->guard_recomputed_slots(), 0, 2 * kGuardSlotBytes, ctx->stream));
+      HIP_CHECK(hipMemcpyAsync(ctx->guard_adapt() + 1, &off, sizeof off, hipMemcpyHostToDevice,
+                               ctx->stream));
       ctx->drain();
       ctx->guard_checked = 0;
     }
