@@ -662,10 +662,10 @@ void run_features_from_raw(eegfx_ctx* ctx, const void* raw, int fmt, int64_t n_f
   if (wide_supported(fmt, ct, C)) {
     void* fscratch = ctx->fused.get(fused_scratch_bytes(n, C));
     HIP_CHECK(launch_baseline_any(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fscratch,
-                                  ctx->err_dev, g.count));
+                                  ctx->err_dev, g.count, fast ? &g : nullptr));
     ctx->tic();
     HIP_CHECK(launch_window_wide(ctx->stream, raw, fmt, n_frames, ct, sel, C, pos, n, fast,
-                                 fscratch, out, g));
+                                 fscratch, out, g, fast && ctx->guard_track()));
     const int64_t elem = fmt == EEGFX_INT_16 ? 2 : 4;
     ctx->toc(n * (EEGFX_DWT8_EPOCH_SIZE * ct * elem + C * 4 + 8 + C * 16 * 8));
     return;

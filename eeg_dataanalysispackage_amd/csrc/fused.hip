@@ -155,27 +155,9 @@ __global__ __launch_bounds__((TILE * C + 63) / 64 * 64) void baseline_kernel(
   const int nt = (n - t0) < TILE ? (int)(n - t0) : TILE;
   // a window kernel that follows may append to the guard list (fma numerics)
   if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
-  // the window kernel's guard strategy for this launch (Guard::adapt): track when the previous
-  // launch sent more than 1/16 of its rows to the second stage.  adapt[1] is the rechecked total
-  // this kernel saw last, as a signed offset (a counter reset on the host subtracts the total it
-  // clears from it, so the difference still counts the launches since)
-  if (adapt && rechecked && blockIdx.x == 0 && tid < 64) {
-    unsigned long long t = 0;
-    for (int i = tid; i < kGuardSlots; i += 64) t += rechecked[i * kGuardSlotWords];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-    if (tid == 0) {
-      const long long delta = (long long)t - (long long)adapt[1];
-      const unsigned long long nprev = adapt[2];
-      unsigned long long mode = adapt[0];
-      if (delta >= 0) mode = nprev > 0 && (unsigned long long)delta * 16 > nprev ? 1ull : 0ull;
-      adapt[0] = mode;
-      adapt[1] = t;
-      adapt[2] = (unsigned long long)n;
-      if (track_out)  // host-mapped: the host launches the next window kernel accordingly
-        __hip_atomic_store(track_out, (unsigned int)mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  // the window kernel's guard strategy for this launch (guard.h guard_adapt_update)
+  if (adapt && rechecked && blockIdx.x == 0 && tid < 64)
+    guard_adapt_update(rechecked, adapt, track_out, n, tid);
   if (tid < TILE) {
     const int64_t p = tid < nt ? pos[t0 + tid] : kPre;
     if (!position_ok(p, n_frames)) flag_position(err);

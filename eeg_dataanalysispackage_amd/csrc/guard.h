@@ -103,6 +103,32 @@ __device__ __forceinline__ bool guard_fails(double acc, double k2, double sum_x2
 __device__ __forceinline__ void guard_slot_add(unsigned long long* slots, unsigned long long v) {
   atomicAdd(slots + (blockIdx.x & (kGuardSlots - 1)) * kGuardSlotWords, v);
 }
+// The window kernel's guard strategy for the launch that follows (Guard::adapt, EEGFX_TRACK_X),
+// by the first wave of a baseline pass's block 0 (lane = tid < 64): track when the previous
+// launch sent more than 1/16 of its rows to the second stage.  adapt[1] is the rechecked total
+// seen last, as a signed offset (a host counter reset subtracts the total it clears, so the
+// difference still counts the launches since); the choice also goes to the host-mapped word the
+// host reads when it picks the window kernel's variant.
+__device__ __forceinline__ void guard_adapt_update(const unsigned long long* rechecked,
+                                                   unsigned long long* adapt,
+                                                   unsigned int* track_out, int64_t n, int lane) {
+  unsigned long long t = 0;
+  for (int i = lane; i < kGuardSlots; i += 64) t += rechecked[i * kGuardSlotWords];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+  if (lane == 0) {
+    const long long delta = (long long)t - (long long)adapt[1];
+    const unsigned long long nprev = adapt[2];
+    unsigned long long mode = adapt[0];
+    if (delta >= 0) mode = nprev > 0 && (unsigned long long)delta * 16 > nprev ? 1ull : 0ull;
+    adapt[0] = mode;
+    adapt[1] = t;
+    adapt[2] = (unsigned long long)n;
+    if (track_out)
+      __hip_atomic_store(track_out, (unsigned int)mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // rows recomputed with the EXACT cascade
 __device__ __forceinline__ void guard_count_recomputed(const Guard& g, unsigned long long rows) {
   guard_slot_add(g.total, rows);

@@ -102,10 +102,12 @@ bool wide_supported(int fmt, int ct, int C);
 bool baseline_any_supported(int fmt, int ct, int C);
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch, int* err, int* guard_count);
+                               void* scratch, int* err, int* guard_count,
+                               const Guard* guard = nullptr);
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                              const void* scratch, double* out, const Guard& guard);
+                              const void* scratch, double* out, const Guard& guard,
+                              bool track = false);
 
 // guard.hip: the EXACT recomputation of the rows the generic any-layout kernels flagged (no-op
 // when g.count is null; launch_window_wide issues it).  raw: the same recording / positions /

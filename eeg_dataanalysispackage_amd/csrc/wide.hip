@@ -43,7 +43,10 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
                                                            int64_t n, int EB, int BSTQ,
                                                            float* __restrict__ bout,
                                                            int* __restrict__ err,
-                                                           int* __restrict__ guard_count) {
+                                                           int* __restrict__ guard_count,
+                                                           const unsigned long long* rechecked,
+                                                           unsigned long long* adapt,
+                                                           unsigned int* track_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t sB[256];
   const int FB = ct * (int)sizeof(T);
@@ -55,6 +58,9 @@ __global__ __launch_bounds__(256) void baseline_any_kernel(const uint8_t* __rest
   const int NQ = BSTQ - 1;  // quads staged per epoch
   // the window kernel that follows appends to the guard list (fma numerics)
   if (guard_count && blockIdx.x == 0 && tid == 0) *guard_count = 0;
+  // the 32-channel window kernel's guard strategy for this launch (guard.h guard_adapt_update)
+  if (adapt && rechecked && blockIdx.x == 0 && tid < 64)
+    guard_adapt_update(rechecked, adapt, track_out, n, tid);
   const int rows = (NQ + 63) / 64;
   if (tid < ne) {
     const int64_t p = pos[e0 + tid];
@@ -369,6 +375,7 @@ struct C32Shared {
   int redo;
   double part[4];     // per-wave sums of squares (EEGFX_C32_REG)
   double gxw[4];      // per-wave sums of the guard's X^2 (EEGFX_C32_REG)
+  double gxm[C32::C];  // measured X_c^2 per channel (the tracking variant, EEGFX_TRACK_X)
 };
 
 // fma numerics, A/B builds: 1 = every lane normalises and stores its own a6, d6 from registers (the row's sum
@@ -393,7 +400,7 @@ __device__ __forceinline__ double wave_sum64(double v) {
 // barrier); this lane's channel c = 8 w + lane / 8 has column col_c, resolution r and baseline b
 // (loaded by the caller, so no memory access of the common path follows a DMA it must not wait
 // for).  Ends with every wave done reading `win` and sh.feat.
-template <bool FAST, bool STREAM>
+template <bool FAST, bool STREAM, bool TRK = false>
 __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int64_t n_frames,
                                             const ChanSel& sel, const float* __restrict__ base,
                                             int64_t e, int64_t B, float b, int col_c, float r,
@@ -407,10 +414,20 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
   const uint8_t* own = eb + 16 * SEGQ * s;
   const uint8_t* nxt = eb + 16 * SEGQ * ((s + 1) & 7);
   double a6, d6;
+  constexpr bool TRACK = FAST && TRK && EEGFX_GUARD;
   if constexpr (FAST) {
 #if EEGFX_COLLAPSED
-    dwt8_collapsed_cascade([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7,
-                           s, a6, d6);
+    float ymax = 0.0f;
+    dwt8_collapsed_cascade<TRACK>([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b,
+                                  lane & ~7, s, a6, d6, &ymax);
+    if constexpr (TRACK) {  // the tracking variant: this channel's measured X_c over its 8 lanes
+      uint32_t u = __float_as_uint(ymax);
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0xB1, 0xF, 0xF, true));
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x4E, 0xF, 0xF, true));
+      u = max(u, (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x141, 0xF, 0xF, true));
+      const double X = (double)__uint_as_float(u);
+      if (s == 0) sh.gxm[c] = X * X;
+    }
 #else
     dwt8_fast_cascade([&](int k) { return sample_at<int16_t>(own + k * FB); }, r, b, lane & ~7, s,
                       a6, d6);
@@ -469,7 +486,13 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
         sx += __shfl_xor(sx, off, 64);
       }
       bool fails = EEGFX_GUARD && guard.total && guard_fails(acc, kGuardK2Collapsed, sx);
-      if (fails) {  // wave-uniform, rare: the second stage on the staged window (still intact)
+      if (TRACK && fails) {  // the second stage from the measured X_c of every channel
+        if (lane == 0) guard_count_rechecked(guard, 1);
+        double sm = lane < C ? sh.gxm[lane] : 0.0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off, 64);
+        fails = guard_fails(acc, kGuardK2Collapsed, sm * (1.0 + 0x1p-20));
+      } else if (fails) {  // wave-uniform, rare: the second stage on the staged window (intact)
         if (lane == 0) guard_count_rechecked(guard, 1);
         fails = guard_fails(
             acc, kGuardK2Collapsed,
@@ -533,7 +556,7 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
   }
 }
 
-template <bool FAST, bool STREAM>
+template <bool FAST, bool STREAM, bool TRK = false>
 __global__ __launch_bounds__(256) void window_c32_kernel(
     const uint8_t* __restrict__ raw, int64_t n_frames, ChanSel sel,
     const int64_t* __restrict__ pos, const float* __restrict__ base, int64_t n,
@@ -548,8 +571,8 @@ __global__ __launch_bounds__(256) void window_c32_kernel(
   const float b = base[e * C32::C + c];
   dma_drain();
   __syncthreads();
-  c32_compute<FAST, STREAM>(raw, n_frames, sel, base, e, B, b, sel.col[c], sel.res[c], win, sh,
-                            out, guard, tid);
+  c32_compute<FAST, STREAM, TRK>(raw, n_frames, sel, base, e, B, b, sel.col[c], sel.res[c], win,
+                                 sh, out, guard, tid);
 }
 
 }  // namespace dev
@@ -599,7 +622,10 @@ bool baseline_any_supported(int fmt, int ct, int C) {
 
 hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                                const ChanSel& sel, int C, const int64_t* pos, int64_t n,
-                               void* scratch, int* err, int* guard_count) {
+                               void* scratch, int* err, int* guard_count, const Guard* guard) {
+  const unsigned long long* rechecked = guard ? guard->rechecked : nullptr;
+  unsigned long long* adapt = guard && guard->total ? guard->adapt : nullptr;
+  unsigned int* track_out = adapt ? guard->track_out : nullptr;
   if (n == 0) return hipSuccess;
   int BSTQ = 0;
   const int EB = baseline_any_tile(fmt, ct, C, &BSTQ);
@@ -608,32 +634,33 @@ hipError_t launch_baseline_any(hipStream_t st, const void* raw, int fmt, int64_t
   if (fmt == 0 && streaming_reads(n_frames, n, dev::kPre + 687))  // pre-stimulus frames unshared
     hipLaunchKernelGGL((dev::baseline_any_kernel<int16_t, true>), grid, dim3(256), lds, st,
                        (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
-                       guard_count);
+                       guard_count, rechecked, adapt, track_out);
   else if (fmt == 0)
     hipLaunchKernelGGL(dev::baseline_any_kernel<int16_t>, grid, dim3(256), lds, st,
                        (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
-                       guard_count);
+                       guard_count, rechecked, adapt, track_out);
   else
     hipLaunchKernelGGL(dev::baseline_any_kernel<float>, grid, dim3(256), lds, st,
                        (const uint8_t*)raw, n_frames, ct, sel, C, pos, n, EB, BSTQ, (float*)scratch, err,
-                       guard_count);
+                       guard_count, rechecked, adapt, track_out);
   return hipGetLastError();
 }
 
 static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, int fmt,
                                              int64_t n_frames, int ct, const ChanSel& sel, int C,
                                              const int64_t* pos, int64_t n, bool fast,
-                                             const void* scratch, double* out, const Guard& guard);
+                                             const void* scratch, double* out, const Guard& guard,
+                                             bool track);
 
 // The generic kernels append the rows that fail the fma guard to the list (their LDS has no room
 // for the recomputation) and the follow-up launch recomputes them (guard.hip); the 32-channel
 // kernel recomputes its own (guard.total only).
 hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t n_frames, int ct,
                               const ChanSel& sel, int C, const int64_t* pos, int64_t n, bool fast,
-                              const void* scratch, double* out, const Guard& guard) {
+                              const void* scratch, double* out, const Guard& guard, bool track) {
   if (n == 0) return hipSuccess;
   const hipError_t e = launch_window_wide_kernels(st, raw, fmt, n_frames, ct, sel, C, pos, n, fast,
-                                                  scratch, out, guard);
+                                                  scratch, out, guard, track);
   if (e != hipSuccess || !fast || !guard.count) return e;
   if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) return hipSuccess;
   return launch_guard_fixup_raw(st, raw, fmt, n_frames, ct, sel, C, pos, scratch, guard, out);
@@ -642,7 +669,8 @@ hipError_t launch_window_wide(hipStream_t st, const void* raw, int fmt, int64_t 
 static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, int fmt,
                                              int64_t n_frames, int ct, const ChanSel& sel, int C,
                                              const int64_t* pos, int64_t n, bool fast,
-                                             const void* scratch, double* out, const Guard& guard) {
+                                             const void* scratch, double* out, const Guard& guard,
+                                             bool track) {
   const float* base = (const float*)scratch;
   const bool two = wide_lds_per_epoch(fmt, ct, C) <= 32 * 1024;  // dynamic LDS stays <= 64 KB
 #define EEGFX_W(T, FA)                                                                        \
@@ -651,11 +679,14 @@ static hipError_t launch_window_wide_kernels(hipStream_t st, const void* raw, in
   if (fmt == 0 && ct == 32 && C == 32 && ((uintptr_t)out & 15) == 0) {  // configs[3]
     const bool nt = streaming_reads(n_frames, n, dev::kWin + 8);
     const dim3 g((unsigned)n);
-#define EEGFX_C32(FA, NTV) \
-    hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV>), g, dim3(256), 0, st, (const uint8_t*)raw, \
-                       n_frames, sel, pos, base, n, out, guard)
-    if (fast) { if (nt) EEGFX_C32(true, true); else EEGFX_C32(true, false); }
-    else { if (nt) EEGFX_C32(false, true); else EEGFX_C32(false, false); }
+#define EEGFX_C32(FA, NTV, TK)                                                              \
+    hipLaunchKernelGGL((dev::window_c32_kernel<FA, NTV, TK>), g, dim3(256), 0, st,           \
+                       (const uint8_t*)raw, n_frames, sel, pos, base, n, out, guard)
+    // the guard's second stage by tracking max |x| (guard.h EEGFX_TRACK_X)
+    const bool trk = EEGFX_TRACK_X != 0 && (EEGFX_TRACK_X == 2 || track) && guard.total;
+    if (fast && trk) { if (nt) EEGFX_C32(true, true, true); else EEGFX_C32(true, false, true); }
+    else if (fast) { if (nt) EEGFX_C32(true, true, false); else EEGFX_C32(true, false, false); }
+    else { if (nt) EEGFX_C32(false, true, false); else EEGFX_C32(false, false, false); }
 #undef EEGFX_C32
     return hipGetLastError();
   }

@@ -343,6 +343,28 @@ def test_guard_strategies_agree():
     c.close()
 
 
+def test_guard_strategies_agree_c32():
+    """The same for the 32-channel kernel (wide.hip window_c32_kernel): its first launch tests the
+    flagged rows against the staged window in one wave, later launches after a heavily flagged one
+    use the X_c every lane tracked while decoding; same rows, counters and oracle values."""
+    c = fx.Context(0, numerics="fma")
+    n = 40
+    raw, pos, flat = flat_recording(n, 1000, 32, 2)
+    cols, res = list(range(32)), [0.1] * 32
+    want = oracle.process_recording(raw, cols, res, pos)
+    runs = []
+    for _ in range(3):
+        c.guard_detail(reset=True)
+        got = c.process_recording(raw, 32, cols, res, pos)
+        runs.append((got, c.guard_detail()))
+    for got, (checked, rechecked, redone) in runs:
+        assert within(got, want)
+        assert checked == n and redone == 0 and rechecked >= len(flat)
+    assert runs[0][1] == runs[1][1] == runs[2][1]
+    assert eq(runs[0][0], runs[1][0]) and eq(runs[1][0], runs[2][0])
+    c.close()
+
+
 def test_exact_numerics_not_guarded():
     c = fx.Context(0)  # EXACT
     raw = alternating(12000, 3, 5, 0)
