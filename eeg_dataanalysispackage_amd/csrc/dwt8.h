@@ -855,46 +855,60 @@ static __constant__ double kHG[2 * kTaps] = {
     EEGFX_H0, EEGFX_H1, EEGFX_H2, EEGFX_H3, EEGFX_H4, EEGFX_H5, EEGFX_H6, EEGFX_H7, EEGFX_H8,
     EEGFX_H9, tap_g(0), tap_g(1), tap_g(2), tap_g(3), tap_g(4), tap_g(5), tap_g(6), tap_g(7),
     tap_g(8), tap_g(9)};
-template <typename Sample>
-__device__ __forceinline__ void dwt8_exact_row_wave(Sample sample, int C, int nfeat,
-                                                    double* scratch, double* row, int lane) {
-  // loops kept rolled and the taps read from kHG: the kernels this is inlined into keep their
-  // register budget (the unrolled form raised the 3-channel window kernel from 44 to 94 VGPRs)
+// One channel of dwt8_exact_row_wave from its 512 decoded doubles in scratch[0, 512) (LDS, this
+// wave's writes synchronised): rowc[k], k < nfeat, receives its unnormalised features; scratch:
+// 768 doubles of LDS no other wave touches.
+__device__ __forceinline__ void dwt8_exact_channel_lds(int nfeat, double* scratch, double* rowc,
+                                                       int lane) {
+  double* in = scratch;
+  double* out = scratch + kWin;
+  int n = kWin;
 #pragma unroll 1
-  for (int c = 0; c < C; ++c) {
-    double* in = scratch;
-    double* out = scratch + kWin;
+  for (int level = 1; level <= 5; ++level) {
 #pragma unroll 1
-    for (int k = lane; k < kWin; k += 64) in[k] = sample(c, k);
-    wave_sync();
-    int n = kWin;
-#pragma unroll 1
-    for (int level = 1; level <= 5; ++level) {
-#pragma unroll 1
-      for (int i = lane; i < n / 2; i += 64) {
-        double a = in[2 * i] * kHG[0];
-#pragma unroll 1
-        for (int j = 1; j < kTaps; ++j) a = a + in[(2 * i + j) & (n - 1)] * kHG[j];
-        out[i] = a;
-      }
-      wave_sync();
-      double* t = in;
-      in = out;
-      out = t;
-      n /= 2;
-    }
-    if (lane < 16) {  // level 6 on the 16 values of a5: a6[i] (lanes 0-7), d6[i] (lanes 8-15)
-      const int i = lane & 7;
-      const double* f = kHG + (lane >= 8 ? kTaps : 0);
-      double a = in[2 * i] * f[0];
-#pragma unroll 1
-      for (int j = 1; j < kTaps; ++j) a = a + in[(2 * i + j) & 15] * f[j];
-      const int k = lane >= 8 ? 8 + i : i;
-      if (k < nfeat) row[c * nfeat + k] = a;
+    for (int i = lane; i < n / 2; i += 64) {
+      double x[kTaps];
+#pragma unroll
+      for (int j = 0; j < kTaps; ++j) x[j] = in[(2 * i + j) & (n - 1)];
+      double a = x[0] * kHG[0];
+#pragma unroll
+      for (int j = 1; j < kTaps; ++j) a = a + x[j] * kHG[j];
+      out[i] = a;
     }
     wave_sync();
+    double* t = in;
+    in = out;
+    out = t;
+    n /= 2;
   }
-  const int F = C * nfeat;
+  if (lane < 16) {  // level 6 on the 16 values of a5: a6[i] (lanes 0-7), d6[i] (lanes 8-15)
+    const int i = lane & 7;
+    const double* f = kHG + (lane >= 8 ? kTaps : 0);
+    double a = in[2 * i] * f[0];
+#pragma unroll 1
+    for (int j = 1; j < kTaps; ++j) a = a + in[(2 * i + j) & 15] * f[j];
+    const int k = lane >= 8 ? 8 + i : i;
+    if (k < nfeat) rowc[k] = a;
+  }
+  wave_sync();
+}
+// dwt8_exact_channel_lds with the samples from sample(k), k < 512, all of a lane's loads issued
+// before the first is used (the path is latency-bound: one window per wave)
+template <typename SampleK>
+__device__ __forceinline__ void dwt8_exact_channel_wave(SampleK sample, int nfeat, double* scratch,
+                                                        double* rowc, int lane) {
+  double v[kWin / 64];
+#pragma unroll
+  for (int q = 0; q < kWin / 64; ++q) v[q] = sample(lane + 64 * q);
+#pragma unroll
+  for (int q = 0; q < kWin / 64; ++q) scratch[lane + 64 * q] = v[q];
+  wave_sync();
+  dwt8_exact_channel_lds(nfeat, scratch, rowc, lane);
+}
+// SignalProcessing.normalize of the F values of `row` (LDS) in place by one wave: sequential sum
+// of squares on lane 0, sqrt, divide; scratch: one double of LDS.
+__device__ __forceinline__ void dwt8_normalise_row_wave(double* row, int F, double* scratch,
+                                                        int lane) {
   if (lane == 0) {
     double acc = 0.0;
 #pragma unroll 1
@@ -906,6 +920,17 @@ __device__ __forceinline__ void dwt8_exact_row_wave(Sample sample, int C, int nf
 #pragma unroll 1
   for (int k = lane; k < F; k += 64) row[k] = row[k] / nv;
   wave_sync();
+}
+template <typename Sample>
+__device__ __forceinline__ void dwt8_exact_row_wave(Sample sample, int C, int nfeat,
+                                                    double* scratch, double* row, int lane) {
+  // loops kept rolled and the taps read from kHG: the kernels this is inlined into keep their
+  // register budget (the unrolled form raised the 3-channel window kernel from 44 to 94 VGPRs)
+#pragma unroll 1
+  for (int c = 0; c < C; ++c)
+    dwt8_exact_channel_wave([&](int k) { return sample(c, k); }, nfeat, scratch, row + c * nfeat,
+                            lane);
+  dwt8_normalise_row_wave(row, C * nfeat, scratch, lane);
 }
 
 // x[0..72): samples [64s, 64s+72) mod 512 of this lane's signal (level-0 slice + halo).

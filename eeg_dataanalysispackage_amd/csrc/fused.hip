@@ -440,7 +440,8 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
   __shared__ __attribute__((aligned(16))) uint32_t win_all[SUBS * kSub * G::ESTR];
   __shared__ double norm_all[SUBS * kSub];
   __shared__ double gx_all[FAST ? SUBS * kSub * C : 1];  // the guard's X^2 per signal (fma)
-  constexpr bool REG = FAST && EEGFX_REG_ROWS;
+  // the REG guard paths synchronise the whole workgroup: one sub-tile only
+  constexpr bool REG = FAST && EEGFX_REG_ROWS && SUBS == 1;
   __shared__ double part_all[REG ? SUBS * kSub * C : 1];  // per-signal sums of squares (REG)
   __shared__ double xs_all[REG ? SUBS * kSub * C : 1];    // measured X_c^2 of flagged rows (REG)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
   double a6 = 0.0, d6 = 0.0;
   // TRK: this launch tracks max |x| (EEGFX_TRACK_X, guard.h) -- a variant of its own, so the
   // scanning launches carry no second filter loop
-  constexpr bool TRACKABLE = FAST && TRK && EEGFX_REG_ROWS && EEGFX_GUARD;
+  constexpr bool TRACKABLE = REG && TRK && EEGFX_GUARD;
   constexpr bool track = TRACKABLE;  // (no flag is raised without guard.total either way)
   float ymax = 0.0f;
   if (SUBS == 1 || ne > 0) {
@@ -559,28 +560,33 @@ __global__ __launch_bounds__(64 * C * SUBS, (5 + SUBS - 1) / SUBS) void window_k
       __builtin_nontemporal_store(a6 * inv, o);
       __builtin_nontemporal_store(d6 * inv, o + 8);
     }
-    if (left && w == 0) {
-      // the guard's rare path: each such row recomputed under EXACT from the recording by wave
-      // 0, the staged windows as scratch (every wave is done with them: the barrier above)
-      double* scratch = (double*)win;
-      double* rowbuf = scratch + 768;
+    if (left) {  // uniform
+      // the guard's rarest path: each such row recomputed under EXACT from the recording, channel
+      // w by wave w (the staged windows as scratch, 768 doubles per wave: every wave is done with
+      // them, the barrier above), then normalised and stored by wave 0
+      double* scratch = (double*)win + w * 768;
+      double* rowbuf = (double*)win + C * 768;
       for (uint64_t f = left; f; f &= f - 1) {
         const int e = (__ffsll((unsigned long long)f) - 1) >> 3;
         const int64_t B = wb[e0 + e] & ~(int64_t)1;  // byte offset of the window
         const int64_t f0 = B / G::FB;
-        dwt8_exact_row_wave(
-            [&](int c, int k) {
-              const float rc = sel.res[c], bc = base[(e0 + e) * C + c];
+        dwt8_exact_channel_wave(
+            [&](int k) {
+              const float bc = base[(e0 + e) * C + w];
               const float v = f0 + k < n_frames
-                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * sel.col[c])
+                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * G::FB + 2 * col)
                                   : 0.0f;
-              float y = v * rc;
+              float y = v * r;
               y = y - bc;
               return (double)y;
             },
-            C, 16, scratch, rowbuf, lane);
-        for (int i = lane; i < F; i += 64) out[(e0 + e) * F + i] = rowbuf[i];
-        wave_sync();
+            16, scratch, rowbuf + w * 16, lane);
+        __syncthreads();
+        if (w == 0) {
+          dwt8_normalise_row_wave(rowbuf, F, scratch, lane);
+          for (int i = lane; i < F; i += 64) out[(e0 + e) * F + i] = rowbuf[i];
+        }
+        __syncthreads();
       }
     }
     return;

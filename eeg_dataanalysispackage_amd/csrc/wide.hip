@@ -514,19 +514,31 @@ __device__ __forceinline__ void c32_compute(const uint8_t* __restrict__ raw, int
       }
     }
     __syncthreads();
-    if (sh.redo) {  // the guard's rare path: wave 0 recomputes the row under EXACT (window LDS free)
-      if (w == 0) {
-        const int64_t f0 = B / FB;
-        dwt8_exact_row_wave(
-            [&](int cc, int k) {
-              const float v = f0 + k < n_frames
-                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * FB + 2 * sel.col[cc])
+    if (sh.redo) {
+      // the guard's rare path: the row recomputed under EXACT, channels w, w+4, ... by wave w (the
+      // window LDS free: 768 doubles of scratch per wave), then normalised by wave 0
+      constexpr int NW = 256 / 64;
+      static_assert(NW * 768 * 8 <= K::EQ * 16, "EXACT scratch fits the window buffer");
+      const int64_t f0 = B / FB;
+      double* scratch = (double*)win + w * 768;
+#pragma unroll 1
+      for (int cc = w; cc < C; cc += NW) {
+        const int col = sel.col[cc];
+        const float rc = sel.res[cc], bc = base[e * C + cc];
+        dwt8_exact_channel_wave(
+            [&](int k) {
+              const float x = f0 + k < n_frames
+                                  ? (float)*(const int16_t*)(raw + B + (int64_t)k * FB + 2 * col)
                                   : 0.0f;
-              float y = v * sel.res[cc];
-              y = y - base[e * C + cc];
+              float y = x * rc;
+              y = y - bc;
               return (double)y;
             },
-            C, 16, (double*)win, feat, lane);
+            16, scratch, feat + cc * 16, lane);
+      }
+      __syncthreads();
+      if (w == 0) {
+        dwt8_normalise_row_wave(feat, F, scratch, lane);
         if (lane == 0) {
           sh.norm1 = 1.0;  // the row is normalised
           guard_count_recomputed(guard, 1ull);
