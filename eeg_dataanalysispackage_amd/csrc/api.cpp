@@ -41,6 +41,11 @@ using namespace eegfx;
 #ifndef EEGFX_SMALL_SPIN_US
 #define EEGFX_SMALL_SPIN_US 30
 #endif
+// A/B only: a small call's waiter past the spin polls its event between 10-us sleeps instead of
+// sleeping in the runtime's blocking-sync wait
+#ifndef EEGFX_SMALL_SLEEP_POLL
+#define EEGFX_SMALL_SLEEP_POLL 0
+#endif
 
 namespace {
 
@@ -274,8 +279,14 @@ struct eegfx_ctx {
     hipError_t e;
     while ((e = hipEventQuery(small_done)) == hipErrorNotReady) {
       if (std::chrono::steady_clock::now() - t0 > kSmallSpin) {
+#if EEGFX_SMALL_SLEEP_POLL
+        while ((e = hipEventQuery(small_done)) == hipErrorNotReady)
+          std::this_thread::sleep_for(std::chrono::microseconds(10));
+        break;
+#else
         HIP_CHECK(hipEventSynchronize(small_done));
         return;
+#endif
       }
     }
     HIP_CHECK(e);
@@ -453,33 +464,51 @@ void mb_release(int dev) {
 }
 
 // Admission of small launched calls (one epoch per call from many threads, no server): at most
-// kSmallCallers per device are inside the runtime at once, the others sleep on a condition
-// variable and are admitted in arrival order (tickets).  Without it 28 threads launching and
-// waiting on one device (Spark local[*] with 32 executor threads, 4 of them on servers) convoyed
-// in the runtime: calls of 42-48 ms (profiles/r06/dropin_gate_ab.log; A/B builds vary the cap).
+// kSmallCallers per device are inside the runtime at once, the others sleep and are admitted in
+// arrival order.  Without it 28 threads launching and waiting on one device (Spark local[*] with
+// 32 executor threads, 4 of them on servers) convoyed in the runtime: calls of 42-48 ms
+// (profiles/r06/dropin_gate_ab.log; A/B builds vary the cap).  A leaving caller hands its place to
+// the first waiter and wakes that thread alone (each waiter sleeps on its own condition variable):
+// a shared one woke every waiter at every exit, ~24 wakeups per call at 32 threads.
 #ifndef EEGFX_SMALL_CALLERS
 #define EEGFX_SMALL_CALLERS 8
 #endif
 constexpr int kSmallCallers = EEGFX_SMALL_CALLERS;
+struct SmallWaiter {
+  std::condition_variable cv;
+  bool admitted = false;
+  SmallWaiter* next = nullptr;
+};
 std::mutex g_small_mu;
-std::condition_variable g_small_cv;
-uint64_t g_small_ticket[kMbMaxDevices] = {};  // tickets issued
-uint64_t g_small_done[kMbMaxDevices] = {};    // calls that have left
+int g_small_inside[kMbMaxDevices] = {};
+SmallWaiter* g_small_head[kMbMaxDevices] = {};  // FIFO of sleeping callers
+SmallWaiter* g_small_tail[kMbMaxDevices] = {};
 struct SmallCallGate {
   int dev;
   explicit SmallCallGate(int d) : dev(d >= 0 && d < kMbMaxDevices ? d : -1) {
     if (dev < 0 || kSmallCallers <= 0) return;
     std::unique_lock<std::mutex> l(g_small_mu);
-    const uint64_t t = g_small_ticket[dev]++;
-    g_small_cv.wait(l, [&] { return t < g_small_done[dev] + (uint64_t)kSmallCallers; });
+    if (!g_small_head[dev] && g_small_inside[dev] < kSmallCallers) {
+      ++g_small_inside[dev];
+      return;
+    }
+    SmallWaiter me;
+    (g_small_tail[dev] ? g_small_tail[dev]->next : g_small_head[dev]) = &me;
+    g_small_tail[dev] = &me;
+    me.cv.wait(l, [&] { return me.admitted; });  // the leaver unlinked us and kept our place
   }
   ~SmallCallGate() {
     if (dev < 0 || kSmallCallers <= 0) return;
-    {
-      std::lock_guard<std::mutex> l(g_small_mu);
-      ++g_small_done[dev];
+    std::lock_guard<std::mutex> l(g_small_mu);
+    SmallWaiter* w = g_small_head[dev];
+    if (!w) {
+      --g_small_inside[dev];
+      return;
     }
-    g_small_cv.notify_all();
+    g_small_head[dev] = w->next;
+    if (!g_small_head[dev]) g_small_tail[dev] = nullptr;
+    w->admitted = true;
+    w->cv.notify_one();  // under the lock: the waiter's frame outlives this call
   }
   SmallCallGate(const SmallCallGate&) = delete;
   SmallCallGate& operator=(const SmallCallGate&) = delete;

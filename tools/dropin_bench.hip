@@ -21,6 +21,8 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <pthread.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -61,6 +63,8 @@ struct Job {
   int rc;
   int mailbox;
   std::vector<double> lat;  // seconds per call
+  std::vector<double> at;   // start of each call (steady clock, s)
+  long tid;                 // the worker's kernel thread id (to match a runtime API trace)
   int resident;             // held a started server at the end of its calls
   pthread_barrier_t* bar;   // every thread starts together and holds its context to the end
 };
@@ -75,6 +79,8 @@ static void* worker(void* arg) {
   for (int i = 0; i < 20; ++i)
     eegfx_extract_features_f64(ctx, g_epochs.data(), 1, 3, 8, 512, 175, 16, out, EEGFX_MEM_HOST);
   j->lat.resize((size_t)j->reps);
+  j->at.resize((size_t)j->reps);
+  j->tid = (long)syscall(SYS_gettid);
   if (j->bar) pthread_barrier_wait(j->bar);
   const double t0 = now_s();
   for (int i = 0; i < j->reps; ++i) {
@@ -82,6 +88,7 @@ static void* worker(void* arg) {
     j->rc |= eegfx_extract_features_f64(ctx, g_epochs.data() + (size_t)(i % 11) * 2250, 1, 3, 8,
                                         512, 175, 16, out, EEGFX_MEM_HOST);
     j->lat[(size_t)i] = now_s() - c0;
+    j->at[(size_t)i] = c0;
   }
   j->per_call = (now_s() - t0) / j->reps;
   int32_t en = 0, res = 0;
@@ -90,6 +97,49 @@ static void* worker(void* arg) {
   if (j->bar) pthread_barrier_wait(j->bar);  // resident_servers counts servers held at once
   eegfx_ctx_destroy(ctx);
   return nullptr;
+}
+// T threads with a context each, started together (barrier) and holding their contexts to the
+// end; per-call latency over all calls.  mailbox: every context asks for a server (at most 4 hold
+// one, the rest serve on the launch path).  The slowest calls go to stderr.
+static void thread_leg(int T, int reps, int mailbox, const char* sep) {
+  std::vector<pthread_t> th((size_t)T);
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, nullptr, (unsigned)T);
+  std::vector<Job> jobs((size_t)T, Job{reps, 0.0, 0, mailbox, {}, {}, 0, 0, &bar});
+  for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
+  double agg = 0, mean = 0;
+  int rc = 0, resident = 0;
+  std::vector<double> all;
+  for (int t = 0; t < T; ++t) {
+    pthread_join(th[(size_t)t], nullptr);
+    agg += 1.0 / jobs[(size_t)t].per_call;
+    mean += jobs[(size_t)t].per_call / T;
+    rc |= jobs[(size_t)t].rc;
+    resident += jobs[(size_t)t].resident;
+    all.insert(all.end(), jobs[(size_t)t].lat.begin(), jobs[(size_t)t].lat.end());
+  }
+  pthread_barrier_destroy(&bar);
+  // the slowest calls (stderr): thread, call index, whether that thread held a server
+  for (int rank = 0; rank < 3; ++rank) {
+    int bt = -1, bi = -1;
+    double bv = -1;
+    for (int t = 0; t < T; ++t)
+      for (size_t i = 0; i < jobs[(size_t)t].lat.size(); ++i)
+        if (jobs[(size_t)t].lat[i] > bv) { bv = jobs[(size_t)t].lat[i]; bt = t; bi = (int)i; }
+    if (bt < 0) break;
+    fprintf(stderr, "%s threads %d slowest #%d: %.1f us (thread %d call %d resident %d tid %ld at_ns %.0f)\n",
+            mailbox ? "mailbox" : "launch", T, rank, bv * 1e6, bt, bi, jobs[(size_t)bt].resident,
+            jobs[(size_t)bt].tid, jobs[(size_t)bt].at[(size_t)bi] * 1e9);
+    jobs[(size_t)bt].lat[(size_t)bi] = -jobs[(size_t)bt].lat[(size_t)bi];
+  }
+  for (int t = 0; t < T; ++t)
+    for (double& v : jobs[(size_t)t].lat) v = v < 0 ? -v : v;
+  std::sort(all.begin(), all.end());
+  printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, ", sep, T,
+         1.0 / mean, agg);
+  if (mailbox) printf("\"resident_servers\": %d, ", resident);
+  printf("\"median_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, \"rc\": %d}",
+         all[all.size() / 2] * 1e6, all[(size_t)(all.size() * 0.99)] * 1e6, all.back() * 1e6, rc);
 }
 
 __global__ void empty_kernel(int* p) {
@@ -177,23 +227,10 @@ int main(int argc, char** argv) {
   printf(" \"launch_floor\": {\"empty_kernel_stream_sync_us\": %.2f, \"empty_kernel_event_spin_us\": %.2f},\n",
          sync_floor.med * 1e6, spin_floor.med * 1e6);
   printf(" \"threads\": {");
-  const int Ts[3] = {2, 4, 8};
-  for (int ti = 0; ti < 3; ++ti) {
-    const int T = Ts[ti];
-    std::vector<pthread_t> th((size_t)T);
-    std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 0, {}, 0, nullptr});
-    for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
-    double agg = 0, mean = 0;
-    int rc = 0;
-    for (int t = 0; t < T; ++t) {
-      pthread_join(th[(size_t)t], nullptr);
-      agg += 1.0 / jobs[(size_t)t].per_call;
-      mean += jobs[(size_t)t].per_call / T;
-      rc |= jobs[(size_t)t].rc;
-    }
-    printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, \"rc\": %d}",
-           ti ? ", " : "", T, 1.0 / mean, agg, rc);
-  }
+  // the launch path alone (no server anywhere), up to Spark local[*] on the box's 16 cores and
+  // twice that
+  const int Ts[5] = {2, 4, 8, 16, 32};
+  for (int ti = 0; ti < 5; ++ti) thread_leg(Ts[ti], reps / 2, 0, ti ? ", " : "");
   printf("},\n");
 
   // the resident server: the same calls without a launch each, rows compared with the launch path
@@ -279,49 +316,9 @@ int main(int argc, char** argv) {
            "\"rows_identical_to_launch_path\": %s, \"threads\": {",
            mb.med * 1e6, mb.p99 * 1e6, 1.0 / mb.med, mb11.med * 1e6, k / mb11.med,
            same ? "true" : "false");
-    // T threads with a context each, every one asking for a server: at most 4 hold one (the
-    // highest-priority queue pool), the rest serve on the launch path; per-call latency over all
+    // every context asking for a server
     const int Tm[5] = {2, 4, 8, 16, 32};
-    for (int ti = 0; ti < 5; ++ti) {
-      const int T = Tm[ti];
-      std::vector<pthread_t> th((size_t)T);
-      pthread_barrier_t bar;
-      pthread_barrier_init(&bar, nullptr, (unsigned)T);
-      std::vector<Job> jobs((size_t)T, Job{reps / 2, 0.0, 0, 1, {}, 0, &bar});
-      for (int t = 0; t < T; ++t) pthread_create(&th[(size_t)t], nullptr, worker, &jobs[(size_t)t]);
-      double agg = 0, mean = 0;
-      int rc = 0, resident = 0;
-      std::vector<double> all;
-      for (int t = 0; t < T; ++t) {
-        pthread_join(th[(size_t)t], nullptr);
-        agg += 1.0 / jobs[(size_t)t].per_call;
-        mean += jobs[(size_t)t].per_call / T;
-        rc |= jobs[(size_t)t].rc;
-        resident += jobs[(size_t)t].resident;
-        all.insert(all.end(), jobs[(size_t)t].lat.begin(), jobs[(size_t)t].lat.end());
-      }
-      pthread_barrier_destroy(&bar);
-      // the slowest calls (stderr): thread, call index, whether that thread held a server
-      for (int rank = 0; rank < 3; ++rank) {
-        int bt = -1, bi = -1;
-        double bv = -1;
-        for (int t = 0; t < T; ++t)
-          for (size_t i = 0; i < jobs[(size_t)t].lat.size(); ++i)
-            if (jobs[(size_t)t].lat[i] > bv) { bv = jobs[(size_t)t].lat[i]; bt = t; bi = (int)i; }
-        if (bt < 0) break;
-        fprintf(stderr, "threads %d slowest #%d: %.1f us (thread %d call %d resident %d)\n", T, rank,
-                bv * 1e6, bt, bi, jobs[(size_t)bt].resident);
-        jobs[(size_t)bt].lat[(size_t)bi] = -jobs[(size_t)bt].lat[(size_t)bi];
-      }
-      for (int t = 0; t < T; ++t)
-        for (double& v : jobs[(size_t)t].lat) v = v < 0 ? -v : v;
-      std::sort(all.begin(), all.end());
-      printf("%s\"%d\": {\"per_thread_epochs_per_s\": %.1f, \"aggregate_epochs_per_s\": %.1f, "
-             "\"resident_servers\": %d, \"median_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, "
-             "\"rc\": %d}",
-             ti ? ", " : "", T, 1.0 / mean, agg, resident, all[all.size() / 2] * 1e6,
-             all[(size_t)(all.size() * 0.99)] * 1e6, all.back() * 1e6, rc);
-    }
+    for (int ti = 0; ti < 5; ++ti) thread_leg(Tm[ti], reps / 2, 1, ti ? ", " : "");
     printf("}},\n");
   }
 
