@@ -41,6 +41,10 @@ using namespace eegfx;
 #ifndef EEGFX_SMALL_SPIN_US
 #define EEGFX_SMALL_SPIN_US 30
 #endif
+// A/B only: configs[4]'s marker positions uploaded beside the first chunk instead of before it
+#ifndef EEGFX_STREAM_POS_AFTER
+#define EEGFX_STREAM_POS_AFTER 0
+#endif
 // A/B only: a small call's waiter past the spin polls its event between 10-us sleeps instead of
 // sleeping in the runtime's blocking-sync wait
 #ifndef EEGFX_SMALL_SLEEP_POLL
@@ -252,15 +256,21 @@ struct eegfx_ctx {
   // streamed path (eegfx_process_recording_streamed): upload / download streams and the chunk
   // events, created on first use and kept for the context's lifetime
   hipStream_t up = nullptr, down = nullptr;
-  static constexpr int kRing = 4;  // device chunk buffers in flight
-  hipEvent_t copied[kRing] = {}, done[kRing] = {};
-  void stream_resources() {
-    if (up) return;
-    HIP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
-    for (int b = 0; b < kRing; ++b) {
-      HIP_CHECK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+  std::vector<hipEvent_t> copied, done;  // per device chunk buffer: uploaded / kernels done
+  void stream_resources(size_t ring) {
+    if (!up) {
+      HIP_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+      HIP_CHECK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+    }
+    while (copied.size() < ring) {
+      hipEvent_t a = nullptr, b = nullptr;
+      HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+      if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        fail(EEGFX_EHIP, "hipEventCreateWithFlags");
+      }
+      copied.push_back(a);
+      done.push_back(b);
     }
   }
   // Completion of a small (latency-bound) call: spinning on an event query returns ~0.5 us sooner
@@ -386,11 +396,10 @@ struct eegfx_ctx {
     release_mailbox();
     if (small_done) (void)hipEventDestroy(small_done);
     small_done = nullptr;
-    for (int b = 0; b < kRing; ++b) {
-      if (copied[b]) (void)hipEventDestroy(copied[b]);
-      if (done[b]) (void)hipEventDestroy(done[b]);
-      copied[b] = done[b] = nullptr;
-    }
+    for (hipEvent_t e : copied) (void)hipEventDestroy(e);
+    for (hipEvent_t e : done) (void)hipEventDestroy(e);
+    copied.clear();
+    done.clear();
     if (up) (void)hipStreamDestroy(up);
     if (down) (void)hipStreamDestroy(down);
     up = down = nullptr;
@@ -1409,25 +1418,17 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
     // copy on the context stream behind the first chunk's frames (7.44-7.48 against 7.13-7.16);
     // each pinned chunk as two halves on two upload streams (7.75-7.81 against 7.14).
     int64_t* d_pos = (int64_t*)ctx->pos.get(sizeof(int64_t) * (size_t)n);
-    HIP_CHECK(hipMemcpyAsync(d_pos, spos, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice,
-                             ctx->stream));
+    auto upload_positions = [&] {
+      HIP_CHECK(hipMemcpyAsync(d_pos, spos, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice,
+                               ctx->stream));
+    };
+    if (!EEGFX_STREAM_POS_AFTER) upload_positions();
     double* d_out = (double*)ctx->out.get(sizeof(double) * (size_t)(n * F));
     (void)ctx->fused.get(fused_scratch_bytes(n, C));  // every chunk's baselines fit: no realloc
     // chunk buffers: 64 B front pad (the kernels round the first quad down by < 16 B) + data
     // (rounded to 256 B so the second buffer is as aligned as the first: the kernels read
     // 16-byte quads relative to `raw`)
     const size_t cbytes = ((size_t)(chunk_frames * FB) + 128 + 255) & ~(size_t)255;
-    constexpr int R = eegfx_ctx::kRing;
-    uint8_t* dbuf = (uint8_t*)ctx->raw.get(R * cbytes);
-    hipPointerAttribute_t attr;
-    const bool pinned = hipPointerGetAttributes(&attr, raw) == hipSuccess &&
-                        attr.type == hipMemoryTypeHost;
-    (void)hipGetLastError();  // a pageable pointer can leave an error behind
-    void* pin[2] = {nullptr, nullptr};
-    ctx->stream_resources();
-    hipStream_t cs = ctx->up, os = ctx->down;  // upload (H2D) and download (D2H) streams
-    hipEvent_t* copied = ctx->copied;
-    hipEvent_t* done = ctx->done;
     // Chunk sizes ramp up (c/4, c/2, then c) and down (about half of what remains, not below
     // c/4) so that the first upload and the last download -- the parts of a call that nothing
     // overlaps -- stay short.
@@ -1438,18 +1439,44 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
       if (rest < 2 * chunk_frames) c = std::min(c, (rest + 1) / 2);
       return std::min(chunk_frames, std::max(c, std::max(chunk_frames / 4, 2 * kSpan)));
     };
+    struct Chunk {
+      int64_t i, j, lo, hi;  // epochs [i, j), frames [lo, hi)
+    };
+    std::vector<Chunk> plan;
+    for (int64_t i = 0; i < n;) {
+      const int64_t lo = spos[i] - EEGFX_PRESTIMULUS;
+      const int64_t hi = std::min(lo + chunk_at((int64_t)plan.size(), lo), n_frames);
+      // the epochs whose span [pos-100, pos+687) ends by hi (all of them at the recording end):
+      // a prefix of the sorted positions, found by bisection (a linear scan of configs[4]'s 576k
+      // positions delayed the first upload by ~150 us)
+      const int64_t j =
+          hi == n_frames ? n
+                         : std::upper_bound(spos + i, spos + n, hi + EEGFX_PRESTIMULUS - kSpan) - spos;
+      plan.push_back({i, j, lo, hi});
+      i = j;
+    }
+    // A ring of 4 device chunk buffers (fewer for fewer chunks).  One buffer per chunk (the whole
+    // 346 MB recording in HBM, no upload ever waiting for an earlier chunk's kernels) measured the
+    // same: 7.16-7.18 against 7.13-7.18 ms (profiles/r06/stream_ring_ab.log).
+    const size_t R = std::min<size_t>(plan.size(), 4);
+    uint8_t* dbuf = (uint8_t*)ctx->raw.get(R * cbytes);
+    hipPointerAttribute_t attr;
+    const bool pinned = hipPointerGetAttributes(&attr, raw) == hipSuccess &&
+                        attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // a pageable pointer can leave an error behind
+    void* pin[2] = {nullptr, nullptr};
+    ctx->stream_resources(std::max<size_t>(R, 2));
+    hipStream_t cs = ctx->up, os = ctx->down;  // upload (H2D) and download (D2H) streams
+    hipEvent_t* copied = ctx->copied.data();
+    hipEvent_t* done = ctx->done.data();
     try {
       if (!pinned) {  // the context's grow-only staging (pinned_pool: growing it syncs nothing)
         for (int b = 0; b < 2; ++b) pin[b] = ctx->pin_chunk[b].get(cbytes);
       }
       ctx->drain();  // d_pos uploaded; buffers idle
-      int64_t i = 0, k = 0;
-      while (i < n) {
-        const int b = (int)(k % R);
-        const int64_t lo = spos[i] - EEGFX_PRESTIMULUS;
-        const int64_t hi = std::min(lo + chunk_at(k, lo), n_frames);
-        int64_t j = i;
-        while (j < n && (spos[j] - EEGFX_PRESTIMULUS + kSpan <= hi || hi == n_frames)) ++j;
+      for (size_t k = 0; k < plan.size(); ++k) {
+        const size_t b = k % R;
+        const int64_t i = plan[k].i, j = plan[k].j, lo = plan[k].lo, hi = plan[k].hi;
         const int64_t Lb = (lo * FB) & ~(int64_t)15, Hb = hi * FB;
         const size_t bytes = Hb > Lb ? (size_t)(Hb - Lb) : 0;
         uint8_t* dst = dbuf + (size_t)b * cbytes + 64;
@@ -1462,6 +1489,7 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
         }
         if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs));
         HIP_CHECK(hipEventRecord(copied[b], cs));
+        if (EEGFX_STREAM_POS_AFTER && k == 0) upload_positions();  // beside the first chunk's
         HIP_CHECK(hipStreamWaitEvent(ctx->stream, copied[b], 0));
         // frame f of the recording lives at raw_dev + f*FB for lo <= f < hi (pointer arithmetic
         // only: nothing below dst is ever read)
@@ -1475,8 +1503,6 @@ int eegfx_process_recording_streamed(eegfx_ctx* ctx, const void* raw, int32_t fm
                                    sizeof(double) * (size_t)((j - i) * F), hipMemcpyDeviceToHost,
                                    os));
         }
-        i = j;
-        ++k;
       }
       if (in_order) {
         HIP_CHECK(hipStreamSynchronize(os));
