@@ -672,6 +672,9 @@ struct Joiner {
 // Host batches up to this many window bytes go through the zero-copy path of
 // eegfx_extract_features_f64 (about 64 epochs of 3 channels).
 constexpr size_t kZeroCopyBytes = (size_t)768 << 10;
+// the rows of the largest such batch: 192 window rows of 512 doubles, 16 features each
+constexpr size_t kZeroCopyOutBytes =
+    kZeroCopyBytes / (sizeof(double) * EEGFX_DWT8_EPOCH_SIZE) * EEGFX_DWT8_FEATURE_SIZE * sizeof(double);
 
 void check_mem(int mem) {
   if (mem != EEGFX_MEM_HOST && mem != EEGFX_MEM_DEVICE) fail(EEGFX_EINVAL, "mem flag %d", mem);
@@ -1067,6 +1070,11 @@ int eegfx_ctx_set_mailbox(eegfx_ctx* ctx, int enable) {
       return;
     }
     if (ctx->mailbox) return;
+    // the small-call staging at its largest before any server is launched on it: a server reads
+    // the buffers it was launched with, so growing them on a later call stopped and restarted it
+    // (with a pinned allocation: the 3-4 ms first calls of tools/mailbox_threads at 16-32 threads)
+    (void)ctx->pin_in.get(kZeroCopyBytes);
+    (void)ctx->pin_out.get(kZeroCopyOutBytes);
     ctx->mailbox = true;  // the server starts on the first one-epoch call that gets a slot
     (void)ctx->mb_ready();
   });

@@ -179,9 +179,10 @@ def test_mailbox_server_slots_at_spark_thread_counts(tmp_path, threads):
     each).  The high-priority queue pool holds 4 servers; a fifth used to share a queue with a
     busy server and wait for it to idle out (1 s) or fail after 30 s.  Now at most 4
     contexts are resident at once, the rest take the launch path, every row equals the launch
-    path's, and no call stalls: the slowest of 6,400 calls at 32 threads stays far below the old
-    1 s queue wait (the bound is loose because the box's 16 host cores are oversubscribed at 32
-    spinning threads; the measured numbers are in DESIGN.md §9)."""
+    path's, and no call stalls.  The small-call staging is allocated when the server is enabled, so
+    no first call grows it and restarts the server (those calls took 3-4 ms at 32 threads); the
+    slowest call measured 0.3-0.8 ms at 32 threads.  The bound here is 10 ms: the
+    box's 16 host cores are shared, and descheduled threads have taken 1-3 ms."""
     import subprocess
     from conftest import DOD01
     exe = _build_mailbox_threads(tmp_path)
@@ -193,4 +194,4 @@ def test_mailbox_server_slots_at_spark_thread_counts(tmp_path, threads):
     f = line.split()
     vals = dict(zip(f[0::2], f[1::2]))
     assert 1 <= int(vals["resident"]) <= 4
-    assert float(vals["max_us"]) < 100_000
+    assert float(vals["max_us"]) < 10_000
