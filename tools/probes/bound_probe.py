@@ -43,6 +43,36 @@ def run(label, reps, up=True, down=True, h_out=h_np, order="ud"):
     print(f"{label:44s} {ms:7.3f} ms per pair (host issue {iss:7.3f} ms)")
 
 
+def chunked(label, up_chunk, down_chunk, down_delay_chunks=0):
+    """both directions as chunked copies queued at once (downloads optionally behind the first
+    `down_delay_chunks` uploads, as the pipeline's rows follow their chunk's kernels)"""
+    fu, fd = flat.view(torch.uint8), h_pin.view(-1).view(torch.uint8)
+    du, dd = d_in.view(torch.uint8), d_out.view(-1).view(torch.uint8)
+    ev = [torch.cuda.Event() for _ in range(64)]
+
+    def go():
+        k = 0
+        for off in range(0, fu.numel(), up_chunk):
+            with torch.cuda.stream(s_in):
+                du[off:off + up_chunk].copy_(fu[off:off + up_chunk], non_blocking=True)
+                ev[k].record(s_in)
+            k += 1
+        for i, off in enumerate(range(0, fd.numel(), down_chunk)):
+            with torch.cuda.stream(s_out):
+                if down_delay_chunks:
+                    s_out.wait_event(ev[min(i + down_delay_chunks, k - 1)])
+                fd[off:off + down_chunk].copy_(dd[off:off + down_chunk], non_blocking=True)
+    go()
+    torch.cuda.synchronize(dev)
+    res = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        go()
+        torch.cuda.synchronize(dev)
+        res.append((time.perf_counter() - t0) * 1e3)
+    print(f"{label:44s} {sorted(res)[1]:7.3f} ms")
+
+
 run("bench leg: numpy view, 5 pairs", 5)
 run("pinned tensor, 5 pairs", 5, h_out=h_pin)
 run("numpy view, 1 pair", 1)
@@ -51,3 +81,6 @@ run("pinned tensor, download issued first, 1 pair", 1, h_out=h_pin, order="du")
 run("upload alone", 1, down=False)
 run("download alone (numpy view)", 1, up=False)
 run("download alone (pinned tensor)", 1, up=False, h_out=h_pin)
+chunked("chunked 48 MB up / 30 MB down, at once", 48 << 20, 30 << 20)
+chunked("chunked, each download behind its upload", 48 << 20, 30 << 20, 1)
+chunked("chunked, each download two uploads behind", 48 << 20, 30 << 20, 2)
