@@ -41,6 +41,10 @@ using namespace eegfx;
 #ifndef EEGFX_SMALL_SPIN_US
 #define EEGFX_SMALL_SPIN_US 30
 #endif
+// A/B only: the small-call admission gate around the launch alone (the wait outside it)
+#ifndef EEGFX_GATE_LAUNCH_ONLY
+#define EEGFX_GATE_LAUNCH_ONLY 0
+#endif
 // A/B only: configs[4]'s marker positions uploaded beside the first chunk instead of before it
 #ifndef EEGFX_STREAM_POS_AFTER
 #define EEGFX_STREAM_POS_AFTER 0
@@ -281,10 +285,13 @@ struct eegfx_ctx {
   // (profiles/r06/dropin_gate_ab.log).
   static constexpr auto kSmallSpin = std::chrono::microseconds(EEGFX_SMALL_SPIN_US);
   hipEvent_t small_done = nullptr;
-  void wait_small() {
+  void record_small() {
     if (!small_done)
       HIP_CHECK(hipEventCreateWithFlags(&small_done, hipEventDisableTiming | hipEventBlockingSync));
     HIP_CHECK(hipEventRecord(small_done, stream));
+  }
+  void wait_small(bool recorded = false) {
+    if (!recorded) record_small();
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
     while ((e = hipEventQuery(small_done)) == hipErrorNotReady) {
@@ -1266,12 +1273,24 @@ int eegfx_extract_features_f64(eegfx_ctx* ctx, const double* epochs, int64_t n, 
           memcpy(out, hout, out_bytes);
           return;
         }
+#if EEGFX_GATE_LAUNCH_ONLY
+        {
+          SmallCallGate gate(ctx->device);
+          ctx->tic();
+          HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n,
+                                          C, feature_size, (double*)ctx->pin_out.device_ptr()));
+          ctx->toc(0);
+          ctx->record_small();
+        }
+        ctx->wait_small(true);
+#else
         SmallCallGate gate(ctx->device);
         ctx->tic();
         HIP_CHECK(launch_features_small(ctx->stream, (const double*)ctx->pin_in.device_ptr(), n, C,
                                         feature_size, (double*)ctx->pin_out.device_ptr()));
         ctx->toc(0);
         ctx->wait_small();
+#endif
         ctx->check_positions_flag();
         memcpy(out, hout, out_bytes);
         return;
