@@ -933,13 +933,26 @@ def bench_stream(args, rank, world, dev, dist):
         with torch.cuda.stream(s_out):
             h_out.copy_(d_out, non_blocking=True)
 
-    copies()
-    torch.cuda.synchronize(dev)
-    c0 = time.perf_counter()
-    for _ in range(5):
-        copies()
-    torch.cuda.synchronize(dev)
-    copy_ms = (time.perf_counter() - c0) / 5 * 1e3
+    def timed_copies(fn, reps=5):
+        fn()
+        torch.cuda.synchronize(dev)
+        c0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - c0) / reps * 1e3
+
+    def upload_only():
+        with torch.cuda.stream(s_in):
+            d_in.copy_(flat, non_blocking=True)
+
+    def download_only():
+        with torch.cuda.stream(s_out):
+            h_out.copy_(d_out, non_blocking=True)
+
+    copy_ms = timed_copies(copies)
+    # each direction alone on this box: the link's rates differ by box
+    up_ms, down_ms = timed_copies(upload_only), timed_copies(download_only)
     del d_in, d_out
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
@@ -961,6 +974,7 @@ def bench_stream(args, rank, world, dev, dist):
             "host_link": {"bound": "pcie", "h2d_GBps": round(h2d, 2),
                           "bytes_per_step": nf * 6, "d2h_bytes_per_step": n * 48 * 8,
                           "copy_only_ms": round(copy_ms, 3),
+                          "upload_alone_ms": round(up_ms, 3), "download_alone_ms": round(down_ms, 3),
                           "frac": round(copy_ms / (el / args.steps * 1e3), 4),
                           "note": "every frame crosses the host link once per step and every "
                                   "feature row once back; copy_only_ms = the same bytes moved by "
